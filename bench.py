@@ -1,0 +1,277 @@
+#!/usr/bin/env python
+"""Benchmark: pixelNeRF coarse + fine ray march (64 + 64 samples) on MI355X.
+
+Workload (BASELINE.json configs[1], "cfg2"): SRN-cars 128x128 frame, 1 source
+view, rendered as 4096-ray chunks x (64 coarse + 64 fine), fp32.  One step =
+one full 128x128 frame (16,384 rays = 4 chunks) through
+``render_par(rays[None])`` exactly as eval/gen_video.py:213-217 drives it.
+Inputs are synthetic (hash-initialised MLP weights and latent) and
+already resident in HBM when the timed region starts.
+
+Multi-GPU (launched by torch.distributed.run): one process per GPU, every rank
+renders its own frame (a different target pose) — weak scaling, no data-path
+collective; a barrier + all_reduce(MAX) of the elapsed time bracket the region.
+
+The JSON line also carries
+  roofline     — the dominant kernel (fine-pass fused point MLP, k_point_mlp):
+                 algorithmic FLOP per launch / its average duration measured with
+                 HIP events recorded on the launch stream inside the timed region,
+                 against the fp32 MFMA peak (157.3 TFLOP/s);
+  composite    — the standalone alpha-composite kernel's HBM roofline (bytes per
+                 ray x rays / duration vs 8 TB/s) on a 1 M-ray batch;
+  cpu_baseline — the CPU oracle (oracle/ref_cpu.py, a restatement of the
+                 reference's PyTorch path) on a bounded sample of the same frame,
+                 timed on this host, rank 0 at N = 1 only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "pixel-nerf_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from pnr import _lib, synth, util  # noqa: E402
+from pnr.models import PixelNeRFNet  # noqa: E402
+from pnr.renderer import NeRFRenderer  # noqa: E402
+
+MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
+FLOP_PER_POINT_NS1 = 4761600 + 2101248   # NS*4,761,600 + 2,101,248
+KC, KF = 64, 64
+CHUNK = 4096
+W = H = 128
+
+
+def model_conf():
+    mlp = dict(type="resnet", n_blocks=5, d_hidden=512, combine_layer=3, combine_type="average")
+    return dict(use_encoder=True, use_xyz=True, use_code=True,
+                code=dict(num_freqs=6, freq_factor=1.5, include_input=True), use_viewdirs=True,
+                use_code_viewdirs=False, mlp_coarse=mlp, mlp_fine=mlp,
+                encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
+
+
+class HipEvents:
+    """hipEvent_t handles from the HIP runtime torch already loaded."""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL("libamdhip64.so.7")
+        self.hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
+                                                 ctypes.c_void_p]
+        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+
+    def create(self, n):
+        evs = []
+        for _ in range(n):
+            e = ctypes.c_void_p()
+            assert self.hip.hipEventCreate(ctypes.byref(e)) == 0
+            evs.append(e)
+        return evs
+
+    def elapsed_ms(self, a, b):
+        ms = ctypes.c_float()
+        rc = self.hip.hipEventElapsedTime(ctypes.byref(ms), a, b)
+        assert rc == 0, rc
+        return ms.value
+
+
+def build_scene(dev, rank):
+    sd = synth.pixelnerf_state(1)
+    net = PixelNeRFNet(model_conf())
+    net.load_state_dict(sd, strict=False)
+    net = net.to(dev).eval()
+    lat = synth.latent(0, 1, 512, 64, 64).to(dev)
+    net.encode_latent(lat, synth.srn_poses([0.0]).to(dev), torch.tensor(131.25, device=dev), (W, H))
+    tgt = synth.srn_poses([30.0 + 15.0 * rank])
+    rays = util.gen_rays(tgt, W, H, torch.tensor(131.25), 0.01, 4.0).reshape(-1, 8).to(dev)
+    return sd, net, rays.contiguous()
+
+
+def cpu_baseline(sd, rays_cpu, n_rays):
+    """Oracle (CPU restatement of the reference path) on a bounded sample."""
+    from oracle import ref_cpu
+
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    scene = ref_cpu.Scene(synth.latent(0, 1, 512, 64, 64), synth.srn_poses([0.0]),
+                          torch.tensor(131.25), W, H, None)
+    rays = rays_cpu[:n_rays][None].contiguous()
+    streams = synth.rng_streams(2, n_rays, KC, KF, 0)
+    fn = lambda p, c, d: ref_cpu.pixelnerf_forward(sd, scene, p, c, d)  # noqa: E731
+    with torch.no_grad():
+        ref_cpu.render(fn, rays[:, :8], KC, KF, 0, tuple(s[:8] for s in streams), True)  # warm-up
+        t0 = time.perf_counter()
+        ref_cpu.render(fn, rays, KC, KF, 0, streams, True)
+        dt = time.perf_counter() - t0
+    return dict(value=round(n_rays / dt, 2), unit="rays/s", cores=torch.get_num_threads(),
+                kind="port",
+                sample="%d rays of the cfg2 frame x (64+64) samples, oracle/ref_cpu.py, %.1f s" % (
+                    n_rays, dt))
+
+
+def composite_roofline(dev, ev):
+    """Standalone composite kernel on 1 M rays x 128 samples (HBM-bound)."""
+    from pnr import ops
+
+    B, K = 1 << 20, 128
+    g = torch.Generator(device=dev).manual_seed(0)
+    rays = torch.zeros(B, 8, device=dev)
+    rays[:, 6] = 0.01
+    rays[:, 7] = 4.0
+    z = torch.sort(torch.rand(B, K, device=dev, generator=g) * 3.9 + 0.05, -1)[0]
+    raw = torch.rand(B, K, 4, device=dev, generator=g)
+    lib = _lib.load()
+    rgb = torch.empty(B, 3, device=dev)
+    depth = torch.empty(B, device=dev)
+    w = torch.empty(B, K, device=dev)
+    st = _lib.stream_of(dev)
+    evs = ev.create(2)
+    res = {}
+    for want_w in (False, True):
+        for _ in range(2):
+            ops.composite(z, raw, rays, True, want_weights=want_w)
+        times = []
+        for _ in range(5):
+            ev.hip.hipEventRecord(evs[0], st)
+            _lib.check(lib.pnr_composite(_lib.ptr(z), _lib.ptr(raw), _lib.ptr(rays), B, K, 1,
+                                         _lib.ptr(w) if want_w else None, _lib.ptr(rgb),
+                                         _lib.ptr(depth), st), "pnr_composite")
+            ev.hip.hipEventRecord(evs[1], st)
+            torch.cuda.synchronize(dev)
+            times.append(ev.elapsed_ms(evs[0], evs[1]))
+        ms = sorted(times)[len(times) // 2]
+        per_ray = 4 * K + 16 * K + 4 + 12 + 4 + (4 * K if want_w else 0)
+        gbs = per_ray * B / (ms * 1e-3) / 1e9
+        res["weights" if want_w else "no_weights"] = dict(
+            ms=round(ms, 4), bytes_per_ray=per_ray, achieved=round(gbs, 1), peak=HBM_PEAK_GBS,
+            unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-rays", type=int, default=2048)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-composite", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    sd, net, rays = build_scene(dev, rank)
+    renderer = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True,
+                            eval_batch_size=CHUNK).to(dev)
+    render_par = renderer.bind_parallel(net, [local], simple_output=True).eval()
+    lib = _lib.load()
+    chunks = list(torch.split(rays, CHUNK, dim=0))
+    ev = HipEvents()
+
+    # instrument the fused render: record events around every kernel of each chunk
+    orig = lib.pnr_render_forward
+    pool = []
+    recording = {"on": False}
+
+    def render_with_events(*a):
+        if not recording["on"]:
+            return orig(*a)
+        evs = ev.create(7)
+        pool.append(evs)
+        arr = (ctypes.c_void_p * 7)(*[e.value for e in evs])
+        return lib.pnr_render_forward_events(*a, arr)
+
+    lib.pnr_render_forward = render_with_events
+
+    def step():
+        frame = []
+        for r in chunks:
+            rgb, _depth = render_par(r[None])
+            frame.append(rgb[0])
+        return torch.cat(frame)
+
+    torch.manual_seed(1234 + rank)
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        recording["on"] = True
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            img = step()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        recording["on"] = False
+        if world > 1:
+            dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert bool(torch.isfinite(img).all())
+
+    # per-kernel durations from the events recorded in the timed region
+    names = ["sample_coarse", "mlp_coarse", "composite_coarse", "sample_fine", "mlp_fine",
+             "composite_fine"]
+    per = {n: [] for n in names}
+    for evs in pool:
+        for i, n in enumerate(names):
+            per[n].append(ev.elapsed_ms(evs[i], evs[i + 1]))
+    avg = {n: sum(v) / len(v) for n, v in per.items()}
+    pts_fine = CHUNK * (KC + KF)
+    flop_fine = pts_fine * FLOP_PER_POINT_NS1
+    achieved = flop_fine / (avg["mlp_fine"] * 1e-3) / 1e12
+
+    rays_total = W * H * args.steps * world
+    value = rays_total / elapsed
+    out = {
+        "metric": "rays/sec (coarse+fine, 64+64 samples)",
+        "value": round(value, 1),
+        "unit": "rays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (hash-initialised ResnetFC weights + latent; SRN geometry)",
+        "config": {"workload": "cfg2: SRN-cars 128x128 frame, 1 source view, 4096-ray chunks x "
+                               "(64 coarse + 64 fine)", "frame": [W, H], "chunk_rays": CHUNK,
+                   "n_coarse": KC, "n_fine": KF, "n_views": 1, "rays_per_step_per_gpu": W * H,
+                   "parallelism": "rays sharded by frame, 1 process per GPU"},
+        "roofline": {"kernel": "k_point_mlp (fine pass)", "bound": "mfma",
+                     "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                     "traffic": None, "flop_per_launch": flop_fine,
+                     "launch_ms": round(avg["mlp_fine"], 4)},
+        "kernel_ms": {n: round(v, 4) for n, v in avg.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_composite:
+        out["composite"] = composite_roofline(dev, ev)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(sd, rays.cpu(), args.cpu_rays)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

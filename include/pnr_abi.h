@@ -1,0 +1,189 @@
+/*
+ * pnr_abi.h — C ABI of the MI355X (gfx950) pixelNeRF ray-march library (libpnr.so).
+ *
+ * The library replaces the per-ray hot path of the reference (etiiiR/pixel-nerf):
+ *   src/render/nerf.py      NeRFRenderer.forward / sample_* / composite  (nerf.py:98-303)
+ *   src/model/models.py     PixelNeRFNet.forward                         (models.py:146-266)
+ *   src/model/resnetfc.py   ResnetFC / ResnetBlockFC                     (resnetfc.py:10-184)
+ *   src/model/code.py       PositionalEncoding                           (code.py:30-42)
+ *   src/model/encoder.py    SpatialEncoder.index (grid_sample)           (encoder.py:80-109)
+ *
+ * Conventions
+ *   - Every pointer is a DEVICE pointer owned by the caller, except the struct
+ *     arguments themselves (host memory, read during the call only).
+ *   - All tensors are fp32, C-contiguous, row-major, in the shapes given below.
+ *   - Calls are asynchronous and stream-ordered on `stream` (a hipStream_t; NULL
+ *     = the default stream).  The library never allocates device memory: scratch
+ *     comes from a caller-provided workspace sized by the *_workspace_bytes query.
+ *   - Functions return PNR_OK (0) or a negative pnr_status; pnr_last_error()
+ *     returns a thread-local message for the last failing call on that thread.
+ *     No C++ exception crosses this boundary.
+ *   - Re-entrant: no mutable global state; callers may use one thread per GPU.
+ */
+#ifndef PNR_ABI_H
+#define PNR_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PNR_ABI_VERSION 1
+
+typedef enum pnr_status {
+    PNR_OK = 0,
+    PNR_ERR_INVALID = -1,     /* bad argument / shape / null pointer               */
+    PNR_ERR_UNSUPPORTED = -2, /* configuration the kernels do not implement        */
+    PNR_ERR_HIP = -3,         /* HIP runtime error (launch or device query)        */
+    PNR_ERR_WORKSPACE = -4    /* workspace missing or too small                    */
+} pnr_status;
+
+typedef void *pnr_stream_t; /* hipStream_t */
+
+/* Encoded source views: what PixelNeRFNet.encode() leaves in the model
+ * (models.py:111-141) plus the encoder feature map (encoder.py:160-163). */
+typedef struct pnr_scene {
+    const float *latent; /* (n_obj*n_views, latent_h, latent_w, latent_c), channels-LAST  */
+    const float *cams;   /* (n_obj*n_views, 16): R_wc[3][3] row-major, t_wc[3],
+                            fx, fy (already negated as models.py:130 does), cx, cy         */
+    int32_t n_obj;       /* SB: objects in the super-batch                                 */
+    int32_t n_views;     /* NS: source views per object                                    */
+    int32_t latent_h, latent_w, latent_c;
+    float image_w, image_h; /* PixelNeRFNet.image_shape = [W, H] (models.py:116-117)       */
+} pnr_scene;
+
+/* Shape of a ResnetFC (resnetfc.py:65-130) + positional encoding (code.py). */
+typedef struct pnr_mlp_desc {
+    int32_t d_in;          /* 42 for the shipped conf (xyz PE 39 + viewdir 3)             */
+    int32_t d_latent;      /* 512                                                          */
+    int32_t d_hidden;      /* 512                                                          */
+    int32_t d_out;         /* 4                                                            */
+    int32_t n_blocks;      /* 5                                                            */
+    int32_t combine_layer; /* 3 (>= n_blocks means never combine; requires n_views == 1)  */
+    int32_t pe_n;          /* entries of code._freqs / code._phases (2*num_freqs = 12)    */
+} pnr_mlp_desc;
+
+/* Unpacked weights in torch nn.Linear layout: weight (out, in), bias (out). */
+typedef struct pnr_mlp_weights {
+    pnr_mlp_desc desc;
+    const float *lin_in_w, *lin_in_b;
+    const float *lin_z_w[8], *lin_z_b[8];  /* min(combine_layer, n_blocks) entries  */
+    const float *fc0_w[8], *fc0_b[8];      /* blocks[i].fc_0, n_blocks entries       */
+    const float *fc1_w[8], *fc1_b[8];      /* blocks[i].fc_1                         */
+    const float *lin_out_w, *lin_out_b;
+    const float *pe_freqs, *pe_phases;     /* code._freqs, code._phases (pe_n each)  */
+} pnr_mlp_weights;
+
+/* Rays, (n_rays, 8) = [ox, oy, oz, dx, dy, dz, near, far] (nerf.py:101).  Rays are
+ * object-major: ray b belongs to object b / rays_per_obj (nerf.py:191-196). */
+typedef struct pnr_rays {
+    const float *rays;
+    int64_t n_rays;
+    int64_t rays_per_obj;
+} pnr_rays;
+
+/* Random streams, drawn in the reference's order (nerf.py:111, 135, 141, 158). */
+typedef struct pnr_rng {
+    const float *u_coarse;   /* (n_rays, n_coarse)          U[0,1)  */
+    const float *u_fine;     /* (n_rays, n_fine - n_fine_depth)     */
+    const float *u_fine_jit; /* (n_rays, n_fine - n_fine_depth)     */
+    const float *n_depth;    /* (n_rays, n_fine_depth)      N(0,1)  */
+} pnr_rng;
+
+typedef struct pnr_render_cfg {
+    int32_t n_coarse;     /* Kc                          (nerf.py:75)       */
+    int32_t n_fine;       /* Kf incl. depth samples       (nerf.py:76)       */
+    int32_t n_fine_depth; /* Kfd                          (nerf.py:77)       */
+    float depth_std;      /*                              (nerf.py:80)       */
+    int32_t white_bkgd;   /*                              (nerf.py:83)       */
+    int32_t lindisp;      /*                              (nerf.py:84)       */
+} pnr_render_cfg;
+
+/* Outputs; any pointer may be NULL except the rgb/depth of each pass that runs. */
+typedef struct pnr_render_out {
+    float *coarse_rgb;     /* (n_rays, 3)                              */
+    float *coarse_depth;   /* (n_rays)                                 */
+    float *coarse_weights; /* (n_rays, n_coarse)                       */
+    float *fine_rgb;       /* (n_rays, 3)           if n_fine > 0      */
+    float *fine_depth;     /* (n_rays)                                 */
+    float *fine_weights;   /* (n_rays, n_coarse + n_fine)              */
+    float *z_coarse;       /* (n_rays, n_coarse)    sample depths      */
+    float *z_fine;         /* (n_rays, n_coarse + n_fine), sorted      */
+} pnr_render_out;
+
+/* ---- library ---------------------------------------------------------------- */
+int pnr_abi_version(void);
+const char *pnr_last_error(void);
+
+/* ---- MLP weight packing (ResnetFC -> MFMA fragment order) ------------------- */
+/* Replaces: the nn.Linear parameters of ResnetFC (resnetfc.py:88-112) as the hot
+ * path consumes them.  Pack once per weight version; the packed buffer is what
+ * pnr_point_query / pnr_render_forward read. */
+size_t pnr_mlp_packed_bytes(const pnr_mlp_desc *desc);
+int pnr_mlp_pack(const pnr_mlp_weights *w, void *packed, size_t packed_bytes,
+                 pnr_stream_t stream);
+
+/* ---- per-point model query ---------------------------------------------------- */
+/* Replaces: PixelNeRFNet.forward(xyz, coarse, viewdirs) (models.py:146-266):
+ * world->camera transform, PE, projection + bilinear latent gather, ResnetFC with
+ * the multi-view mean, sigmoid/relu head.  xyz/viewdirs (n_obj*points_per_obj, 3);
+ * viewdirs may be NULL (zeros).  out (n_obj*points_per_obj, 4). */
+size_t pnr_point_query_workspace_bytes(const pnr_scene *scene, int64_t n_points);
+int pnr_point_query(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                    const float *xyz, const float *viewdirs, int64_t points_per_obj,
+                    float *out, void *workspace, size_t workspace_bytes,
+                    pnr_stream_t stream);
+
+/* ---- full coarse + fine render ------------------------------------------------ */
+/* Replaces: NeRFRenderer.forward(model, rays, want_weights) (nerf.py:251-303)
+ * with model = PixelNeRFNet (mlp_coarse / mlp_fine; pass the coarse pack twice when
+ * mlp_fine is None, models.py:242). */
+size_t pnr_render_workspace_bytes(const pnr_scene *scene, const pnr_render_cfg *cfg,
+                                  int64_t n_rays);
+int pnr_render_forward(const pnr_scene *scene, const pnr_mlp_desc *desc,
+                       const void *coarse_packed, const void *fine_packed,
+                       const pnr_rays *rays, const pnr_rng *rng,
+                       const pnr_render_cfg *cfg, const pnr_render_out *out,
+                       void *workspace, size_t workspace_bytes, pnr_stream_t stream);
+
+/* Same as pnr_render_forward, plus hipEventRecord of caller-created events on
+ * `stream` around every launch: events[0] before sample_coarse, [1] after it
+ * (= before the coarse point MLP), [2] after the coarse MLP, [3] after the coarse
+ * composite, [4] after sample_fine, [5] after the fine MLP, [6] after the fine
+ * composite (entries 4-6 unused when n_fine == 0).  `events` holds 7 hipEvent_t;
+ * no host synchronization is added.  Used by bench.py for per-kernel timing. */
+int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
+                              const void *coarse_packed, const void *fine_packed,
+                              const pnr_rays *rays, const pnr_rng *rng,
+                              const pnr_render_cfg *cfg, const pnr_render_out *out,
+                              void *workspace, size_t workspace_bytes, pnr_stream_t stream,
+                              void *const *events);
+
+/* ---- building blocks (also the generic model-callback path) ------------------ */
+/* Replaces: NeRFRenderer.sample_coarse (nerf.py:98-118).  z (n_rays, n_coarse). */
+int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse,
+                      const float *u_coarse, int32_t lindisp, float *z,
+                      pnr_stream_t stream);
+
+/* Replaces: sample_fine + sample_fine_depth + cat + sort (nerf.py:120-161, 284-295).
+ * weights/depth of the coarse pass; z_fine (n_rays, n_coarse + n_fine) sorted. */
+int pnr_sample_fine(const float *rays, int64_t n_rays, int32_t n_coarse,
+                    const float *z_coarse, const float *coarse_weights,
+                    const float *coarse_depth, int32_t n_fine, int32_t n_fine_depth,
+                    float depth_std, const float *u_fine, const float *u_fine_jit,
+                    const float *n_depth, int32_t lindisp, float *z_fine,
+                    pnr_stream_t stream);
+
+/* Replaces: NeRFRenderer.composite's alpha compositing (nerf.py:176-249).
+ * z (n_rays, K), raw (n_rays, K, 4) = model output [r, g, b, sigma];
+ * weights (n_rays, K) may be NULL; rgb (n_rays, 3); depth (n_rays). */
+int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n_rays,
+                  int32_t k, int32_t white_bkgd, float *weights, float *rgb, float *depth,
+                  pnr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PNR_ABI_H */

@@ -1,0 +1,262 @@
+// extern "C" entry points of libpnr.so (declared in include/pnr_abi.h):
+// argument validation, workspace carving and the stream-ordered launch
+// sequence of the coarse + fine ray march.  No allocation, no host sync.
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "pnr_common.h"
+
+namespace pnr {
+
+// launchers (march.hip, mlp.hip)
+int launch_sample_coarse(const float *, int64_t, int, const float *, int, float *, hipStream_t);
+int launch_sample_fine(const float *, int64_t, int, const float *, const float *, const float *,
+                       int, int, float, const float *, const float *, const float *, int, float *,
+                       hipStream_t);
+int launch_composite(const float *, const float *, const float *, int64_t, int, int, float *,
+                     float *, float *, hipStream_t);
+size_t mlp_packed_bytes(const pnr_mlp_desc &);
+int mlp_check_desc(const pnr_mlp_desc &);
+int mlp_pack(const pnr_mlp_weights &, void *, size_t, hipStream_t);
+size_t mlp_xsum_bytes(int ns);
+int launch_point_mlp(const pnr_scene &, const pnr_mlp_desc &, const void *, const float *,
+                     const float *, int, int64_t, const float *, const float *, int64_t, int64_t,
+                     float *, float *, hipStream_t);
+
+static thread_local char g_err[1024];
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int fail(int status, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return status;
+}
+
+int device_cu_count() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v > 0) return v;
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        n = 256;
+    cache[dev].store(n, std::memory_order_relaxed);
+    return n;
+}
+
+static size_t align_up(size_t v) { return (v + 255) & ~(size_t)255; }
+
+static int check_scene(const pnr_scene *sc) {
+    if (!sc) return fail(PNR_ERR_INVALID, "scene is NULL");
+    if (!sc->latent || !sc->cams) return fail(PNR_ERR_INVALID, "scene latent/cams NULL");
+    if (sc->n_obj < 1 || sc->n_views < 1) return fail(PNR_ERR_INVALID, "n_obj/n_views < 1");
+    if (sc->latent_h < 2 || sc->latent_w < 2)
+        return fail(PNR_ERR_INVALID, "latent must be at least 2x2 (align_corners scaling)");
+    if (sc->latent_c != 512) return fail(PNR_ERR_UNSUPPORTED, "latent_c must be 512 (got %d)", sc->latent_c);
+    if (!(sc->image_w > 0.f) || !(sc->image_h > 0.f)) return fail(PNR_ERR_INVALID, "image size <= 0");
+    if ((reinterpret_cast<uintptr_t>(sc->latent) & 15) != 0)
+        return fail(PNR_ERR_INVALID, "latent must be 16-byte aligned");
+    return PNR_OK;
+}
+
+static int check_desc_for_scene(const pnr_mlp_desc *d, const pnr_scene *sc) {
+    if (!d) return fail(PNR_ERR_INVALID, "mlp desc is NULL");
+    int rc = mlp_check_desc(*d);
+    if (rc) return rc;
+    if (sc->n_views > 1 && d->combine_layer >= d->n_blocks)
+        return fail(PNR_ERR_UNSUPPORTED, "n_views > 1 needs combine_layer < n_blocks");
+    return PNR_OK;
+}
+
+}  // namespace pnr
+
+using namespace pnr;
+
+extern "C" {
+
+int pnr_abi_version(void) { return PNR_ABI_VERSION; }
+
+const char *pnr_last_error(void) { return g_err; }
+
+size_t pnr_mlp_packed_bytes(const pnr_mlp_desc *desc) {
+    if (!desc || mlp_check_desc(*desc) != PNR_OK) return 0;
+    return mlp_packed_bytes(*desc);
+}
+
+int pnr_mlp_pack(const pnr_mlp_weights *w, void *packed, size_t packed_bytes, pnr_stream_t stream) {
+    if (!w || !packed) return fail(PNR_ERR_INVALID, "pnr_mlp_pack: NULL argument");
+    return mlp_pack(*w, packed, packed_bytes, (hipStream_t)stream);
+}
+
+size_t pnr_point_query_workspace_bytes(const pnr_scene *scene, int64_t n_points) {
+    (void)n_points;
+    return scene ? align_up(mlp_xsum_bytes(scene->n_views)) : 0;
+}
+
+int pnr_point_query(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                    const float *xyz, const float *viewdirs, int64_t points_per_obj, float *out,
+                    void *workspace, size_t workspace_bytes, pnr_stream_t stream) {
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    if ((rc = check_desc_for_scene(desc, scene))) return rc;
+    if (!packed || !xyz || !out) return fail(PNR_ERR_INVALID, "pnr_point_query: NULL pointer");
+    if (points_per_obj < 0) return fail(PNR_ERR_INVALID, "points_per_obj < 0");
+    const int64_t n_points = points_per_obj * scene->n_obj;
+    if (n_points == 0) return PNR_OK;
+    const size_t need = pnr_point_query_workspace_bytes(scene, n_points);
+    if (need && (!workspace || workspace_bytes < need))
+        return fail(PNR_ERR_WORKSPACE, "pnr_point_query: workspace %zu < %zu", workspace_bytes, need);
+    return launch_point_mlp(*scene, *desc, packed, nullptr, nullptr, 0, 1, xyz, viewdirs,
+                            points_per_obj, n_points, out, static_cast<float *>(workspace),
+                            (hipStream_t)stream);
+}
+
+// workspace layout of pnr_render_forward
+struct RenderWs {
+    size_t z_c, raw_c, w_c, z_f, raw_f, xsum, total;
+};
+
+static RenderWs render_ws(const pnr_scene *sc, const pnr_render_cfg *cfg, int64_t n) {
+    RenderWs w;
+    const size_t kc = (size_t)cfg->n_coarse, kall = (size_t)(cfg->n_coarse + cfg->n_fine);
+    size_t o = 0;
+    w.z_c = o; o += align_up(sizeof(float) * n * kc);
+    w.raw_c = o; o += align_up(sizeof(float) * n * kc * 4);
+    w.w_c = o; o += align_up(sizeof(float) * n * kc);
+    w.z_f = o; o += cfg->n_fine > 0 ? align_up(sizeof(float) * n * kall) : 0;
+    w.raw_f = o; o += cfg->n_fine > 0 ? align_up(sizeof(float) * n * kall * 4) : 0;
+    w.xsum = o; o += align_up(mlp_xsum_bytes(sc->n_views));
+    w.total = o;
+    return w;
+}
+
+size_t pnr_render_workspace_bytes(const pnr_scene *scene, const pnr_render_cfg *cfg, int64_t n_rays) {
+    if (!scene || !cfg || n_rays < 0) return 0;
+    return render_ws(scene, cfg, n_rays).total;
+}
+
+int pnr_render_forward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *coarse_packed,
+                       const void *fine_packed, const pnr_rays *rays, const pnr_rng *rng,
+                       const pnr_render_cfg *cfg, const pnr_render_out *out, void *workspace,
+                       size_t workspace_bytes, pnr_stream_t stream) {
+    return pnr_render_forward_events(scene, desc, coarse_packed, fine_packed, rays, rng, cfg, out,
+                                     workspace, workspace_bytes, stream, nullptr);
+}
+
+int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
+                              const void *coarse_packed, const void *fine_packed,
+                              const pnr_rays *rays, const pnr_rng *rng, const pnr_render_cfg *cfg,
+                              const pnr_render_out *out, void *workspace, size_t workspace_bytes,
+                              pnr_stream_t stream, void *const *events) {
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    if ((rc = check_desc_for_scene(desc, scene))) return rc;
+    if (!rays || !rng || !cfg || !out) return fail(PNR_ERR_INVALID, "pnr_render_forward: NULL struct");
+    if (!coarse_packed) return fail(PNR_ERR_INVALID, "coarse_packed is NULL");
+    const int kc = cfg->n_coarse, kf = cfg->n_fine, kfd = cfg->n_fine_depth;
+    if (kc < 1) return fail(PNR_ERR_INVALID, "n_coarse < 1");
+    if (kf < 0 || kfd < 0 || kfd > kf) return fail(PNR_ERR_INVALID, "need 0 <= n_fine_depth <= n_fine");
+    if (kc + kf > 1024) return fail(PNR_ERR_UNSUPPORTED, "n_coarse + n_fine must be <= 1024");
+    if (kf > 0 && !fine_packed) return fail(PNR_ERR_INVALID, "fine_packed is NULL");
+    const int64_t n = rays->n_rays;
+    if (n < 0 || !rays->rays) return fail(PNR_ERR_INVALID, "bad rays");
+    if (n == 0) return PNR_OK;
+    if (rays->rays_per_obj <= 0 || n % rays->rays_per_obj != 0 || n / rays->rays_per_obj != scene->n_obj)
+        return fail(PNR_ERR_INVALID, "n_rays (%lld) must be n_obj (%d) x rays_per_obj (%lld)",
+                    (long long)n, scene->n_obj, (long long)rays->rays_per_obj);
+    if (!rng->u_coarse) return fail(PNR_ERR_INVALID, "u_coarse stream is NULL");
+    if (kf - kfd > 0 && (!rng->u_fine || !rng->u_fine_jit)) return fail(PNR_ERR_INVALID, "fine streams NULL");
+    if (kfd > 0 && !rng->n_depth) return fail(PNR_ERR_INVALID, "n_depth stream NULL");
+    if (!out->coarse_rgb || !out->coarse_depth) return fail(PNR_ERR_INVALID, "coarse outputs NULL");
+    if (kf > 0 && (!out->fine_rgb || !out->fine_depth)) return fail(PNR_ERR_INVALID, "fine outputs NULL");
+    const RenderWs w = render_ws(scene, cfg, n);
+    if (!workspace || workspace_bytes < w.total)
+        return fail(PNR_ERR_WORKSPACE, "pnr_render_forward: workspace %zu < %zu", workspace_bytes, w.total);
+    char *ws = static_cast<char *>(workspace);
+    hipStream_t st = (hipStream_t)stream;
+    float *zc = out->z_coarse ? out->z_coarse : reinterpret_cast<float *>(ws + w.z_c);
+    float *rawc = reinterpret_cast<float *>(ws + w.raw_c);
+    float *wc = out->coarse_weights ? out->coarse_weights : reinterpret_cast<float *>(ws + w.w_c);
+    float *xsum = reinterpret_cast<float *>(ws + w.xsum);
+    auto mark = [&](int i) -> int {
+        if (!events || !events[i]) return PNR_OK;
+        hipError_t e = hipEventRecord((hipEvent_t)events[i], st);
+        return e == hipSuccess ? PNR_OK : fail(PNR_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
+    };
+
+    // coarse pass (nerf.py:273-276)
+    if ((rc = mark(0))) return rc;
+    if ((rc = launch_sample_coarse(rays->rays, n, kc, rng->u_coarse, cfg->lindisp, zc, st))) return rc;
+    if ((rc = mark(1))) return rc;
+    if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj,
+                               nullptr, nullptr, 1, n * kc, rawc, xsum, st)))
+        return rc;
+    if ((rc = mark(2))) return rc;
+    if ((rc = launch_composite(zc, rawc, rays->rays, n, kc, cfg->white_bkgd, wc, out->coarse_rgb,
+                               out->coarse_depth, st)))
+        return rc;
+    if ((rc = mark(3))) return rc;
+    if (kf == 0) return PNR_OK;
+    // fine pass (nerf.py:284-301)
+    const int kall = kc + kf;
+    float *zf = out->z_fine ? out->z_fine : reinterpret_cast<float *>(ws + w.z_f);
+    float *rawf = reinterpret_cast<float *>(ws + w.raw_f);
+    if ((rc = launch_sample_fine(rays->rays, n, kc, zc, wc, out->coarse_depth, kf, kfd, cfg->depth_std,
+                                 rng->u_fine, rng->u_fine_jit, rng->n_depth, cfg->lindisp, zf, st)))
+        return rc;
+    if ((rc = mark(4))) return rc;
+    if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, zf, kall, rays->rays_per_obj,
+                               nullptr, nullptr, 1, n * kall, rawf, xsum, st)))
+        return rc;
+    if ((rc = mark(5))) return rc;
+    if ((rc = launch_composite(zf, rawf, rays->rays, n, kall, cfg->white_bkgd, out->fine_weights,
+                               out->fine_rgb, out->fine_depth, st)))
+        return rc;
+    return mark(6);
+}
+
+int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse, const float *u_coarse,
+                      int32_t lindisp, float *z, pnr_stream_t stream) {
+    if (n_rays < 0 || n_coarse < 1) return fail(PNR_ERR_INVALID, "pnr_sample_coarse: bad sizes");
+    if (n_rays > 0 && (!rays || !u_coarse || !z)) return fail(PNR_ERR_INVALID, "pnr_sample_coarse: NULL");
+    return launch_sample_coarse(rays, n_rays, n_coarse, u_coarse, lindisp, z, (hipStream_t)stream);
+}
+
+int pnr_sample_fine(const float *rays, int64_t n_rays, int32_t n_coarse, const float *z_coarse,
+                    const float *coarse_weights, const float *coarse_depth, int32_t n_fine,
+                    int32_t n_fine_depth, float depth_std, const float *u_fine,
+                    const float *u_fine_jit, const float *n_depth, int32_t lindisp, float *z_fine,
+                    pnr_stream_t stream) {
+    if (n_rays < 0 || n_coarse < 1 || n_fine < 1 || n_fine_depth < 0 || n_fine_depth > n_fine)
+        return fail(PNR_ERR_INVALID, "pnr_sample_fine: bad sizes");
+    if (n_coarse + n_fine > 1024) return fail(PNR_ERR_UNSUPPORTED, "n_coarse + n_fine must be <= 1024");
+    if (n_rays == 0) return PNR_OK;
+    if (!rays || !z_coarse || !coarse_weights || !z_fine) return fail(PNR_ERR_INVALID, "pnr_sample_fine: NULL");
+    if (n_fine - n_fine_depth > 0 && (!u_fine || !u_fine_jit)) return fail(PNR_ERR_INVALID, "fine streams NULL");
+    if (n_fine_depth > 0 && (!n_depth || !coarse_depth)) return fail(PNR_ERR_INVALID, "depth inputs NULL");
+    return launch_sample_fine(rays, n_rays, n_coarse, z_coarse, coarse_weights, coarse_depth, n_fine,
+                              n_fine_depth, depth_std, u_fine, u_fine_jit, n_depth, lindisp, z_fine,
+                              (hipStream_t)stream);
+}
+
+int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n_rays, int32_t k,
+                  int32_t white_bkgd, float *weights, float *rgb, float *depth, pnr_stream_t stream) {
+    if (n_rays < 0 || k < 1) return fail(PNR_ERR_INVALID, "pnr_composite: bad sizes");
+    if (n_rays == 0) return PNR_OK;
+    if (!z || !raw || !rays || !rgb || !depth) return fail(PNR_ERR_INVALID, "pnr_composite: NULL");
+    if ((reinterpret_cast<uintptr_t>(raw) & 15) != 0) return fail(PNR_ERR_INVALID, "raw must be 16-byte aligned");
+    return launch_composite(z, raw, rays, n_rays, k, white_bkgd, weights, rgb, depth, (hipStream_t)stream);
+}
+
+}  // extern "C"

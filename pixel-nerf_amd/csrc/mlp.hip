@@ -1,0 +1,495 @@
+// Fused per-point pixelNeRF model on gfx950 f32 MFMA.
+//
+// Replaces PixelNeRFNet.forward (models.py:146-266) for the shipped conf:
+//   world->camera transform (162-165), positional encoding (code.py:30-42),
+//   view directions (184-196), pinhole projection + bilinear border gather of
+//   the encoder latent (206-221, encoder.py:80-109), ResnetFC (resnetfc.py:132-184)
+//   with the multi-view mean at combine_layer (util.py:461-471), and the
+//   sigmoid/relu head (258-265).
+//
+// Work decomposition:
+//   * a workgroup = 4 waves (one per SIMD) = a tile of 64 points ("columns").
+//   * every layer is OUT^T (512 x 64) = W (512 x K) * IN^T (K x 64) on
+//     v_mfma_f32_16x16x4_f32.  Wave w owns output rows [128w, 128w+128) for all
+//     64 columns: 8 row tiles x 4 column tiles = 32 accumulators (128 regs).
+//   * IN^T lives in ONE LDS buffer [column][k] (64 x (512+4) fp32 = 132 KB) that
+//     is reused in turn for the PE features, the gathered latent z, relu(x) and
+//     relu(h); B fragments are ds_read_b128 (4 consecutive k of one column).
+//   * W is pre-packed (k_pack) in fragment order [k-block][row tile][lane][4] so
+//     every wave streams its own 8 row tiles with 16-byte coalesced loads straight
+//     into VGPRs, one k-block (16 k) ahead of the MFMAs.  x (the residual stream)
+//     and h stay in accumulator registers for the whole network.
+#include "pnr_common.h"
+
+namespace pnr {
+namespace mlpk {
+
+constexpr int H = 512;             // d_hidden == d_latent (only width implemented)
+constexpr int NRT = H / 16;        // 32 row tiles per layer
+constexpr int NKB = H / 16;        // 32 k-blocks (16 k each) for K = 512
+constexpr int NKB_IN = 4;          // lin_in k-blocks (d_in <= 64, zero padded)
+constexpr int WAVES = 4;
+constexpr int RTW = NRT / WAVES;   // 8 row tiles per wave
+constexpr int CT = 4;              // column tiles (16 columns each)
+constexpr int COLS = 16 * CT;      // 64 points per tile
+constexpr int LDS_LD = H + 4;      // floats per column in the LDS activation buffer
+constexpr int KB_FLOATS = NRT * 256;          // one k-block of a packed layer (32 KB)
+constexpr int LAYER_FLOATS = NKB * KB_FLOATS; // one packed 512x512 layer (1 MB)
+constexpr int HDR = 64;            // header floats: pe freqs [0,16), phases [16,32)
+
+struct Layout {
+    int n_linz, n_l512, n_blocks, ncomb, d_in, d_out, pe_n;
+    int64_t off_lin_in, off_l512, off_lin_out, off_bias, nbias, total;
+};
+
+inline Layout make_layout(const pnr_mlp_desc &d) {
+    Layout L;
+    L.n_blocks = d.n_blocks;
+    L.n_linz = d.combine_layer < d.n_blocks ? d.combine_layer : d.n_blocks;
+    L.ncomb = L.n_linz;
+    L.n_l512 = L.n_linz + 2 * d.n_blocks;
+    L.d_in = d.d_in;
+    L.d_out = d.d_out;
+    L.pe_n = d.pe_n;
+    L.off_lin_in = HDR;
+    L.off_l512 = L.off_lin_in + (int64_t)NKB_IN * KB_FLOATS;
+    L.off_lin_out = L.off_l512 + (int64_t)L.n_l512 * LAYER_FLOATS;
+    L.off_bias = L.off_lin_out + (int64_t)NKB * 256;
+    L.nbias = (int64_t)(1 + L.n_l512) * H + 16;
+    L.total = ((L.off_bias + L.nbias + 63) / 64) * 64;
+    return L;
+}
+
+// packed L512 layer index of block `blk`, kind 0 = lin_z, 1 = fc_0, 2 = fc_1
+__host__ __device__ inline int layer_index(int blk, int kind, int n_linz) {
+    return blk < n_linz ? 3 * blk + kind : 3 * n_linz + 2 * (blk - n_linz) + (kind - 1);
+}
+
+struct PackSrc {
+    const float *lin_in_w, *lin_in_b, *lin_out_w, *lin_out_b, *pe_f, *pe_p;
+    const float *w[24], *b[24];
+};
+
+// One thread per packed float.  Fragment element (kb, rt, lane, s) holds
+// W[16 rt + (lane & 15)][16 kb + 4 (lane >> 4) + s]: the A operand of k-step
+// (kb, s) for row tile rt (v_mfma_f32_16x16x4_f32: lane l holds A[l&15][l>>4]).
+__global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L.total) return;
+    float v = 0.0f;
+    if (i < HDR) {
+        if (i < 16 && i < L.pe_n) v = s.pe_f[i];
+        else if (i >= 16 && i < 32 && (i - 16) < L.pe_n) v = s.pe_p[i - 16];
+    } else if (i < L.off_l512) {
+        const int e = (int)(i - L.off_lin_in);
+        const int kb = e / KB_FLOATS, rt = (e / 256) % NRT, lane = (e >> 2) & 63, j = e & 3;
+        const int row = 16 * rt + (lane & 15), col = 16 * kb + 4 * (lane >> 4) + j;
+        if (col < L.d_in) v = s.lin_in_w[(int64_t)row * L.d_in + col];
+    } else if (i < L.off_lin_out) {
+        const int64_t r = i - L.off_l512;
+        const int layer = (int)(r / LAYER_FLOATS);
+        const int e = (int)(r % LAYER_FLOATS);
+        const int kb = e / KB_FLOATS, rt = (e / 256) % NRT, lane = (e >> 2) & 63, j = e & 3;
+        const int row = 16 * rt + (lane & 15), col = 16 * kb + 4 * (lane >> 4) + j;
+        v = s.w[layer][(int64_t)row * H + col];
+    } else if (i < L.off_bias) {
+        const int e = (int)(i - L.off_lin_out);
+        const int kb = e >> 8, lane = (e >> 2) & 63, j = e & 3;
+        const int row = lane & 15, col = 16 * kb + 4 * (lane >> 4) + j;
+        if (row < L.d_out) v = s.lin_out_w[(int64_t)row * H + col];
+    } else {
+        const int64_t r = i - L.off_bias;
+        const int64_t nb = (int64_t)(1 + L.n_l512) * H;
+        if (r < H) v = s.lin_in_b[r];
+        else if (r < nb) v = s.b[r / H - 1][r % H];
+        else if (r - nb < L.d_out) v = s.lin_out_b[r - nb];
+    }
+    out[i] = v;
+}
+
+// ------------------------------------------------------------------------------
+struct Args {
+    const float *packed;
+    Layout L;
+    // points: render mode (rays + z) or query mode (xyz + dirs)
+    int render_mode;
+    const float *rays, *zs;
+    int K;
+    int64_t rays_per_obj;
+    const float *xyz, *dirs;
+    int64_t points_per_obj;
+    int64_t n_points;
+    // scene
+    const float *latent, *cams;
+    int ns, hl, wl;
+    float img_w, img_h;
+    float *out;
+    float *xsum;       // ns > 1: gridDim.x * COLS * H floats
+    int64_t n_tiles;
+};
+
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+typedef f4 Acc[RTW][CT];
+
+// acc[r][c] (+)= W(rows of this wave) * IN^T over nkb k-blocks.
+//   wp  : this layer's packed weights, already offset to this wave's first row
+//         tile and this lane (stride KB_FLOATS per k-block, 256 per row tile)
+//   inb : LDS activation buffer, already offset to this lane's (column, k) slot
+// Software pipeline: k-block kb+1's A (8 x f4) and B (4 x f4) are loaded while
+// kb's 128 MFMAs issue.
+template <int NK>
+__device__ __forceinline__ void gemm(Acc &acc, const float *__restrict__ wp, const float *inb) {
+    f4 A[RTW], B[CT];
+#pragma unroll
+    for (int r = 0; r < RTW; ++r) A[r] = *reinterpret_cast<const f4 *>(wp + r * 256);
+#pragma unroll
+    for (int c = 0; c < CT; ++c) B[c] = *reinterpret_cast<const f4 *>(inb + c * 16 * LDS_LD);
+#pragma unroll 2
+    for (int kb = 0; kb < NK; ++kb) {
+        f4 An[RTW], Bn[CT];
+        const int kn = kb + 1 < NK ? kb + 1 : kb;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+            An[r] = *reinterpret_cast<const f4 *>(wp + (int64_t)kn * KB_FLOATS + r * 256);
+#pragma unroll
+        for (int c = 0; c < CT; ++c)
+            Bn[c] = *reinterpret_cast<const f4 *>(inb + c * 16 * LDS_LD + kn * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+                for (int r = 0; r < RTW; ++r) acc[r][c] = mfma(A[r][j], B[c][j], acc[r][c]);
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) A[r] = An[r];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) B[c] = Bn[c];
+    }
+}
+
+// acc = bias (per output row) [+ acc]
+__device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bias, int wave, int g,
+                                         bool accumulate) {
+#pragma unroll
+    for (int r = 0; r < RTW; ++r) {
+        const f4 b = *reinterpret_cast<const f4 *>(bias + 16 * (RTW * wave + r) + 4 * g);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[r][c] = accumulate ? acc[r][c] + b : b;
+    }
+}
+
+// IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane)
+__device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const f4 v = acc[r][c];
+            f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+            *reinterpret_cast<f4 *>(inbuf + (16 * c + cl) * LDS_LD + 16 * (RTW * wave + r) + 4 * g) = o;
+        }
+}
+
+__global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *inbuf = smem;                   // COLS x LDS_LD
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4;
+    const int cl = lane & 15;
+    const Layout &L = a.L;
+    const float *bias = a.packed + L.off_bias;
+    const float *pe_f = a.packed;        // code._freqs  (pack header)
+    const float *pe_p = a.packed + 16;   // code._phases
+
+    // per-lane fragment bases
+    const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;
+    const float *inb = inbuf + cl * LDS_LD + 4 * g;     // B: column 16c + cl, k 16kb + 4g
+    // feature / gather role: thread -> (column col, quarter qt)
+    const int col = tid >> 2, qt = tid & 3;
+
+    Acc x, h;
+    for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        const int64_t p_raw = tile * COLS + col;
+        const int64_t p = p_raw < a.n_points ? p_raw : a.n_points - 1;
+        float px, py, pz, dx, dy, dz;
+        int64_t obj;
+        if (a.render_mode) {
+            const int64_t b = p / a.K;
+            const float *ray = a.rays + b * 8;
+            const float zz = a.zs[p];
+            dx = ray[3]; dy = ray[4]; dz = ray[5];
+            // points = o + z * d  (nerf.py:185)
+            px = add_rn(ray[0], mul_rn(zz, dx));
+            py = add_rn(ray[1], mul_rn(zz, dy));
+            pz = add_rn(ray[2], mul_rn(zz, dz));
+            obj = b / a.rays_per_obj;
+        } else {
+            px = a.xyz[p * 3 + 0]; py = a.xyz[p * 3 + 1]; pz = a.xyz[p * 3 + 2];
+            if (a.dirs) { dx = a.dirs[p * 3 + 0]; dy = a.dirs[p * 3 + 1]; dz = a.dirs[p * 3 + 2]; }
+            else { dx = dy = dz = 0.f; }
+            obj = p / a.points_per_obj;
+        }
+        float *xs = a.xsum + (int64_t)(blockIdx.x * WAVES + wave) * (RTW * CT * 256) + lane * 4;
+
+        for (int v = 0; v < a.ns; ++v) {
+            // ---- per (point, view) geometry (this thread's column) ----------------
+            const float *cam = a.cams + (obj * a.ns + v) * 16;
+            float xr[3], vd[3], xc[3];
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                const float r0 = cam[3 * i], r1 = cam[3 * i + 1], r2 = cam[3 * i + 2];
+                xr[i] = add_rn(add_rn(mul_rn(r0, px), mul_rn(r1, py)), mul_rn(r2, pz));
+                vd[i] = add_rn(add_rn(mul_rn(r0, dx), mul_rn(r1, dy)), mul_rn(r2, dz));
+                xc[i] = add_rn(xr[i], cam[9 + i]);
+            }
+            const float fx = cam[12], fy = cam[13], cx = cam[14], cy = cam[15];
+            // features f = 16 qt .. 16 qt + 15 of [xyz_rot | PE | viewdir_cam | 0]
+            __syncthreads();   // previous users of inbuf are done
+            {
+                const int npe = 3 * L.pe_n;
+                float fv[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int f = 16 * qt + i;
+                    float val = 0.f;
+                    if (f < 3) val = xr[f];
+                    else if (f < 3 + npe) {
+                        const int m = f - 3, q = m / 3, d = m - 3 * q;
+                        const float xd = d == 0 ? xr[0] : (d == 1 ? xr[1] : xr[2]);
+                        val = sinf(add_rn(pe_p[q], mul_rn(xd, pe_f[q])));
+                    } else if (f < 6 + npe) {
+                        const int d = f - 3 - npe;
+                        val = d == 0 ? vd[0] : (d == 1 ? vd[1] : vd[2]);
+                    }
+                    fv[i] = val;
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + 16 * qt + 4 * i) =
+                        f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
+            }
+            // projection (models.py:206-212) -> grid_sample coords (encoder.py:95-108)
+            float u = mul_rn(__fdiv_rn(-xc[0], xc[2]), fx);
+            float w = mul_rn(__fdiv_rn(-xc[1], xc[2]), fy);
+            u = add_rn(u, cx);
+            w = add_rn(w, cy);
+            const float wlf = (float)a.wl, hlf = (float)a.hl;
+            const float lsx = mul_rn(__fdiv_rn(wlf, sub_rn(wlf, 1.f)), 2.f);
+            const float lsy = mul_rn(__fdiv_rn(hlf, sub_rn(hlf, 1.f)), 2.f);
+            const float gx = sub_rn(mul_rn(u, __fdiv_rn(lsx, a.img_w)), 1.f);
+            const float gy = sub_rn(mul_rn(w, __fdiv_rn(lsy, a.img_h)), 1.f);
+            float ix = mul_rn(add_rn(gx, 1.f), mul_rn(sub_rn(wlf, 1.f), 0.5f));
+            float iy = mul_rn(add_rn(gy, 1.f), mul_rn(sub_rn(hlf, 1.f), 0.5f));
+            ix = fminf(fmaxf(ix, 0.f), wlf - 1.f);   // border padding; NaN -> 0
+            iy = fminf(fmaxf(iy, 0.f), hlf - 1.f);
+            const float x0f = floorf(ix), y0f = floorf(iy);
+            const float we = sub_rn(ix, x0f), wn = sub_rn(iy, y0f);
+            const float ee = sub_rn(1.f, we), ss = sub_rn(1.f, wn);
+            float wnw = mul_rn(ss, ee), wne = mul_rn(ss, we), wsw = mul_rn(wn, ee), wse = mul_rn(wn, we);
+            const int x0 = (int)x0f, y0 = (int)y0f;
+            const int x1 = x0 + 1 < a.wl ? x0 + 1 : x0, y1 = y0 + 1 < a.hl ? y0 + 1 : y0;
+            if (x0 + 1 >= a.wl) { wne = 0.f; wse = 0.f; }
+            if (y0 + 1 >= a.hl) { wsw = 0.f; wse = 0.f; }
+            const float *lat = a.latent + (obj * a.ns + v) * (int64_t)a.hl * a.wl * H + 128 * qt;
+            const f4 *cnw = reinterpret_cast<const f4 *>(lat + ((int64_t)y0 * a.wl + x0) * H);
+            const f4 *cne = reinterpret_cast<const f4 *>(lat + ((int64_t)y0 * a.wl + x1) * H);
+            const f4 *csw = reinterpret_cast<const f4 *>(lat + ((int64_t)y1 * a.wl + x0) * H);
+            const f4 *cse = reinterpret_cast<const f4 *>(lat + ((int64_t)y1 * a.wl + x1) * H);
+            __syncthreads();   // features visible
+            // ---- lin_in ---------------------------------------------------------------
+            add_bias(x, bias, wave, g, false);
+            gemm<NKB_IN>(x, a.packed + L.off_lin_in + wl_off, inb);
+            // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
+            for (int blk = 0; blk < L.ncomb; ++blk) {
+                const int lz = layer_index(blk, 0, L.ncomb);
+                __syncthreads();
+                // z = bilinear latent gather (torch's nw, ne, sw, se summation order),
+                // channels [128 qt, 128 qt + 128) of this thread's column
+#pragma unroll 4
+                for (int m = 0; m < 32; ++m) {
+                    const f4 c0 = cnw[m], c1 = cne[m], c2 = csw[m], c3 = cse[m];
+                    f4 zz;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        zz[j] = add_rn(add_rn(add_rn(mul_rn(c0[j], wnw), mul_rn(c1[j], wne)),
+                                              mul_rn(c2[j], wsw)), mul_rn(c3[j], wse));
+                    *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + 128 * qt + 4 * m) = zz;
+                }
+                __syncthreads();
+                add_bias(x, bias + (1 + lz) * H, wave, g, true);
+                gemm<NKB>(x, a.packed + L.off_l512 + (int64_t)lz * LAYER_FLOATS + wl_off, inb);
+                __syncthreads();
+                store_relu(x, inbuf, wave, lane);
+                __syncthreads();
+                add_bias(h, bias + (2 + lz) * H, wave, g, false);
+                gemm<NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * LAYER_FLOATS + wl_off, inb);
+                __syncthreads();
+                store_relu(h, inbuf, wave, lane);
+                __syncthreads();
+                add_bias(x, bias + (3 + lz) * H, wave, g, true);
+                gemm<NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * LAYER_FLOATS + wl_off, inb);
+            }
+            // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
+            if (a.ns > 1) {
+                if (v == 0) {
+#pragma unroll
+                    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+                        for (int c = 0; c < CT; ++c)
+                            *reinterpret_cast<f4 *>(xs + (r * CT + c) * 256) = x[r][c];
+                } else if (v < a.ns - 1) {
+#pragma unroll
+                    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+                        for (int c = 0; c < CT; ++c) {
+                            f4 *ptr = reinterpret_cast<f4 *>(xs + (r * CT + c) * 256);
+                            *ptr = *ptr + x[r][c];
+                        }
+                } else {
+                    const float nsf = (float)a.ns;
+#pragma unroll
+                    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+                        for (int c = 0; c < CT; ++c) {
+                            const f4 sum = *reinterpret_cast<const f4 *>(xs + (r * CT + c) * 256) + x[r][c];
+                            x[r][c] = sum / nsf;
+                        }
+                }
+            }
+        }
+        // ---- blocks after the combine layer ------------------------------------------
+        for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
+            const int l0 = layer_index(blk, 1, L.ncomb);
+            __syncthreads();
+            store_relu(x, inbuf, wave, lane);
+            __syncthreads();
+            add_bias(h, bias + (1 + l0) * H, wave, g, false);
+            gemm<NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * LAYER_FLOATS + wl_off, inb);
+            __syncthreads();
+            store_relu(h, inbuf, wave, lane);
+            __syncthreads();
+            add_bias(x, bias + (2 + l0) * H, wave, g, true);
+            gemm<NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * LAYER_FLOATS + wl_off, inb);
+        }
+        // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w -> columns 16w..
+        __syncthreads();
+        store_relu(x, inbuf, wave, lane);
+        __syncthreads();
+        {
+            const float *wo = a.packed + L.off_lin_out + lane * 4;
+            const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
+            f4 o0 = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * g);
+            f4 o1 = {0.f, 0.f, 0.f, 0.f}, o2 = o1, o3 = o1;
+#pragma unroll 4
+            for (int kb = 0; kb < NKB; ++kb) {
+                const f4 wv = *reinterpret_cast<const f4 *>(wo + kb * 256);
+                const f4 bv = *reinterpret_cast<const f4 *>(bi + kb * 16);
+                o0 = mfma(wv.x, bv.x, o0);
+                o1 = mfma(wv.y, bv.y, o1);
+                o2 = mfma(wv.z, bv.z, o2);
+                o3 = mfma(wv.w, bv.w, o3);
+            }
+            const f4 o = (o0 + o1) + (o2 + o3);
+            const int64_t po = tile * COLS + 16 * wave + cl;
+            if (g == 0 && po < a.n_points) {
+                f4 r;
+                r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
+                r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
+                r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
+                r.w = fmaxf(o.w, 0.f);
+                *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+            }
+        }
+    }
+}
+
+}  // namespace mlpk
+
+// ------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------
+size_t mlp_packed_bytes(const pnr_mlp_desc &d) {
+    return sizeof(float) * (size_t)mlpk::make_layout(d).total;
+}
+
+int mlp_check_desc(const pnr_mlp_desc &d) {
+    if (d.d_hidden != mlpk::H || d.d_latent != mlpk::H)
+        return fail(PNR_ERR_UNSUPPORTED, "fused MLP implements d_hidden = d_latent = 512 (got %d, %d)",
+                    d.d_hidden, d.d_latent);
+    if (d.d_out != 4) return fail(PNR_ERR_UNSUPPORTED, "d_out must be 4 (got %d)", d.d_out);
+    if (d.n_blocks < 1 || d.n_blocks > 8) return fail(PNR_ERR_UNSUPPORTED, "n_blocks in [1, 8] (got %d)", d.n_blocks);
+    if (d.combine_layer < 0) return fail(PNR_ERR_INVALID, "combine_layer < 0");
+    if (d.pe_n < 0 || d.pe_n > 16) return fail(PNR_ERR_UNSUPPORTED, "pe_n in [0, 16] (got %d)", d.pe_n);
+    if (d.d_in != 3 + 3 * d.pe_n + 3)
+        return fail(PNR_ERR_UNSUPPORTED, "d_in must be 3 + 3*pe_n + 3 (xyz PE + raw viewdirs); got %d", d.d_in);
+    if (d.d_in > 16 * mlpk::NKB_IN) return fail(PNR_ERR_UNSUPPORTED, "d_in <= 64");
+    return PNR_OK;
+}
+
+int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t st) {
+    const pnr_mlp_desc &d = w.desc;
+    int rc = mlp_check_desc(d);
+    if (rc) return rc;
+    mlpk::Layout L = mlpk::make_layout(d);
+    if (bytes < sizeof(float) * (size_t)L.total) return fail(PNR_ERR_WORKSPACE, "packed buffer too small");
+    mlpk::PackSrc s = {};
+    s.lin_in_w = w.lin_in_w; s.lin_in_b = w.lin_in_b;
+    s.lin_out_w = w.lin_out_w; s.lin_out_b = w.lin_out_b;
+    s.pe_f = w.pe_freqs; s.pe_p = w.pe_phases;
+    if (!s.lin_in_w || !s.lin_in_b || !s.lin_out_w || !s.lin_out_b || (d.pe_n && (!s.pe_f || !s.pe_p)))
+        return fail(PNR_ERR_INVALID, "null weight pointer");
+    for (int blk = 0; blk < d.n_blocks; ++blk) {
+        for (int kind = 0; kind < 3; ++kind) {
+            if (kind == 0 && blk >= L.n_linz) continue;
+            const int li = mlpk::layer_index(blk, kind, L.n_linz);
+            const float *wp = kind == 0 ? w.lin_z_w[blk] : kind == 1 ? w.fc0_w[blk] : w.fc1_w[blk];
+            const float *bp = kind == 0 ? w.lin_z_b[blk] : kind == 1 ? w.fc0_b[blk] : w.fc1_b[blk];
+            if (!wp || !bp) return fail(PNR_ERR_INVALID, "null weight pointer (block %d kind %d)", blk, kind);
+            s.w[li] = wp;
+            s.b[li] = bp;
+        }
+    }
+    const int64_t blocks = (L.total + 255) / 256;
+    hipLaunchKernelGGL(mlpk::k_pack, dim3((unsigned)blocks), dim3(256), 0, st, s, L,
+                       static_cast<float *>(packed));
+    return launch_ok("mlp_pack") ? PNR_OK : PNR_ERR_HIP;
+}
+
+size_t mlp_xsum_bytes(int ns) {
+    if (ns <= 1) return 0;
+    return sizeof(float) * (size_t)device_cu_count() * mlpk::COLS * mlpk::H;
+}
+
+// Launch the fused model over n_points points (render mode if rays != nullptr).
+int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *packed,
+                     const float *rays, const float *zs, int K, int64_t rays_per_obj,
+                     const float *xyz, const float *dirs, int64_t points_per_obj,
+                     int64_t n_points, float *out, float *xsum_ws, hipStream_t st) {
+    if (n_points == 0) return PNR_OK;
+    mlpk::Args a = {};
+    a.packed = static_cast<const float *>(packed);
+    a.L = mlpk::make_layout(d);
+    a.render_mode = rays != nullptr;
+    a.rays = rays; a.zs = zs; a.K = K; a.rays_per_obj = rays_per_obj;
+    a.xyz = xyz; a.dirs = dirs; a.points_per_obj = points_per_obj;
+    a.n_points = n_points;
+    a.latent = sc.latent; a.cams = sc.cams;
+    a.ns = sc.n_views; a.hl = sc.latent_h; a.wl = sc.latent_w;
+    a.img_w = sc.image_w; a.img_h = sc.image_h;
+    a.out = out;
+    a.xsum = xsum_ws;
+    a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
+    const int cus = device_cu_count();
+    const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
+    const size_t lds = sizeof(float) * (size_t)mlpk::COLS * mlpk::LDS_LD;
+    hipLaunchKernelGGL(mlpk::k_point_mlp, dim3((unsigned)grid), dim3(256), lds, st, a);
+    return launch_ok("point_mlp") ? PNR_OK : PNR_ERR_HIP;
+}
+
+}  // namespace pnr

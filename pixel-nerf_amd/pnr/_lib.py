@@ -1,0 +1,124 @@
+"""ctypes binding of libpnr.so (include/pnr_abi.h).
+
+The product path has no fallback: if the HIP library is missing or fails to load,
+every call raises.  ``torch`` is imported first so that the HIP runtime torch
+ships (soname libamdhip64.so.7) is the one libpnr.so binds to.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime before libpnr.so)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpnr.so")
+
+c_f = ctypes.c_float
+c_i32 = ctypes.c_int32
+c_i64 = ctypes.c_int64
+c_size = ctypes.c_size_t
+c_vp = ctypes.c_void_p
+PF = ctypes.POINTER(ctypes.c_float)
+
+
+class Scene(ctypes.Structure):
+    _fields_ = [("latent", c_vp), ("cams", c_vp), ("n_obj", c_i32), ("n_views", c_i32),
+                ("latent_h", c_i32), ("latent_w", c_i32), ("latent_c", c_i32),
+                ("image_w", c_f), ("image_h", c_f)]
+
+
+class MlpDesc(ctypes.Structure):
+    _fields_ = [("d_in", c_i32), ("d_latent", c_i32), ("d_hidden", c_i32), ("d_out", c_i32),
+                ("n_blocks", c_i32), ("combine_layer", c_i32), ("pe_n", c_i32)]
+
+
+class MlpWeights(ctypes.Structure):
+    _fields_ = [("desc", MlpDesc), ("lin_in_w", c_vp), ("lin_in_b", c_vp),
+                ("lin_z_w", c_vp * 8), ("lin_z_b", c_vp * 8),
+                ("fc0_w", c_vp * 8), ("fc0_b", c_vp * 8),
+                ("fc1_w", c_vp * 8), ("fc1_b", c_vp * 8),
+                ("lin_out_w", c_vp), ("lin_out_b", c_vp),
+                ("pe_freqs", c_vp), ("pe_phases", c_vp)]
+
+
+class Rays(ctypes.Structure):
+    _fields_ = [("rays", c_vp), ("n_rays", c_i64), ("rays_per_obj", c_i64)]
+
+
+class Rng(ctypes.Structure):
+    _fields_ = [("u_coarse", c_vp), ("u_fine", c_vp), ("u_fine_jit", c_vp), ("n_depth", c_vp)]
+
+
+class RenderCfg(ctypes.Structure):
+    _fields_ = [("n_coarse", c_i32), ("n_fine", c_i32), ("n_fine_depth", c_i32),
+                ("depth_std", c_f), ("white_bkgd", c_i32), ("lindisp", c_i32)]
+
+
+class RenderOut(ctypes.Structure):
+    _fields_ = [("coarse_rgb", c_vp), ("coarse_depth", c_vp), ("coarse_weights", c_vp),
+                ("fine_rgb", c_vp), ("fine_depth", c_vp), ("fine_weights", c_vp),
+                ("z_coarse", c_vp), ("z_fine", c_vp)]
+
+
+# name -> (restype, argtypes); must match include/pnr_abi.h exactly
+SIGNATURES = {
+    "pnr_abi_version": (c_i32, []),
+    "pnr_last_error": (ctypes.c_char_p, []),
+    "pnr_mlp_packed_bytes": (c_size, [ctypes.POINTER(MlpDesc)]),
+    "pnr_mlp_pack": (c_i32, [ctypes.POINTER(MlpWeights), c_vp, c_size, c_vp]),
+    "pnr_point_query_workspace_bytes": (c_size, [ctypes.POINTER(Scene), c_i64]),
+    "pnr_point_query": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp, c_vp, c_vp,
+                                c_i64, c_vp, c_vp, c_size, c_vp]),
+    "pnr_render_workspace_bytes": (c_size, [ctypes.POINTER(Scene), ctypes.POINTER(RenderCfg), c_i64]),
+    "pnr_render_forward": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp, c_vp,
+                                   ctypes.POINTER(Rays), ctypes.POINTER(Rng),
+                                   ctypes.POINTER(RenderCfg), ctypes.POINTER(RenderOut), c_vp,
+                                   c_size, c_vp]),
+    "pnr_render_forward_events": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp, c_vp,
+                                          ctypes.POINTER(Rays), ctypes.POINTER(Rng),
+                                          ctypes.POINTER(RenderCfg), ctypes.POINTER(RenderOut),
+                                          c_vp, c_size, c_vp, ctypes.POINTER(c_vp)]),
+    "pnr_sample_coarse": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
+    "pnr_sample_fine": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f, c_vp,
+                                c_vp, c_vp, c_i32, c_vp, c_vp]),
+    "pnr_composite": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+}
+
+_lib = None
+
+
+class PnrError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libpnr.so once; raise loudly if it is missing (no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PnrError("libpnr.so not built (%s); run `make -C pixel-nerf_amd` or "
+                       "__graft_entry__.build()" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = load().pnr_last_error().decode(errors="replace")
+        raise PnrError("%s failed (status %d): %s" % (what, rc, msg))
+
+
+def ptr(t):
+    """Device pointer of a tensor (or None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

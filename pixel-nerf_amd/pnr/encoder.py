@@ -1,0 +1,176 @@
+"""Image encoder that produces the latent the ray march gathers from.
+
+Mirrors the interface of the reference's ``SpatialEncoder`` (encoder.py:13-177):
+a ResNet34 trunk (conv1 .. layer3 used; layer4 present for checkpoint
+compatibility), every stage upsampled to the conv1 resolution and concatenated
+into a 512-channel feature map (``num_layers = 4``).  The trunk is defined here
+with torchvision-compatible parameter names (``encoder.model.layer1.0.conv1.weight``
+...) because torchvision is absent offline; it runs on PyTorch-ROCm (MIOpen) once
+per scene and is not part of the per-ray hot path.
+
+The hot path consumes the latent channels-LAST; ``latent_cl`` keeps that copy.
+"""
+import warnings
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+__all__ = ["SpatialEncoder", "resnet34_trunk"]
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, inplanes, planes, stride=1, downsample=None, norm_layer=nn.BatchNorm2d):
+        super().__init__()
+        self.conv1 = nn.Conv2d(inplanes, planes, 3, stride, 1, bias=False)
+        self.bn1 = norm_layer(planes)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(planes, planes, 3, 1, 1, bias=False)
+        self.bn2 = norm_layer(planes)
+        self.downsample = downsample
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idt)
+
+
+class ResNetTrunk(nn.Module):
+    def __init__(self, layers=(3, 4, 6, 3), norm_layer=nn.BatchNorm2d):
+        super().__init__()
+        self.inplanes = 64
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = norm_layer(64)
+        self.relu = nn.ReLU(inplace=True)
+        self.maxpool = nn.MaxPool2d(3, 2, 1)
+        self.layer1 = self._make(64, layers[0], 1, norm_layer)
+        self.layer2 = self._make(128, layers[1], 2, norm_layer)
+        self.layer3 = self._make(256, layers[2], 2, norm_layer)
+        self.layer4 = self._make(512, layers[3], 2, norm_layer)
+        self.avgpool = nn.Sequential()
+        self.fc = nn.Sequential()
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, (nn.BatchNorm2d, nn.GroupNorm)):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+
+    def _make(self, planes, blocks, stride, norm_layer):
+        down = None
+        if stride != 1 or self.inplanes != planes:
+            down = nn.Sequential(nn.Conv2d(self.inplanes, planes, 1, stride, bias=False),
+                                 norm_layer(planes))
+        layers = [BasicBlock(self.inplanes, planes, stride, down, norm_layer)]
+        self.inplanes = planes
+        layers += [BasicBlock(planes, planes, norm_layer=norm_layer) for _ in range(1, blocks)]
+        return nn.Sequential(*layers)
+
+
+def resnet34_trunk(pretrained=False, norm_layer=nn.BatchNorm2d):
+    if pretrained:
+        warnings.warn("pnr: ImageNet ResNet34 weights cannot be downloaded offline; the "
+                      "encoder starts from random init (load a pixelNeRF checkpoint instead)")
+    return ResNetTrunk(norm_layer=norm_layer)
+
+
+def _norm_layer(norm_type):
+    if norm_type == "batch":
+        return nn.BatchNorm2d
+    if norm_type == "instance":
+        return lambda c: nn.InstanceNorm2d(c, affine=False, track_running_stats=False)
+    if norm_type == "group":
+        return lambda c: nn.GroupNorm(32, c)
+    raise NotImplementedError("normalization layer [%s] is not found" % norm_type)
+
+
+class SpatialEncoder(nn.Module):
+    """Pixel-aligned encoder (encoder.py:13-177)."""
+
+    def __init__(self, backbone="resnet34", pretrained=True, num_layers=4, index_interp="bilinear",
+                 index_padding="border", upsample_interp="bilinear", feature_scale=1.0,
+                 use_first_pool=True, norm_type="batch"):
+        super().__init__()
+        if backbone != "resnet34":
+            raise NotImplementedError("pnr SpatialEncoder implements backbone=resnet34 only")
+        if index_interp != "bilinear" or index_padding != "border":
+            raise NotImplementedError("the HIP gather implements bilinear / border indexing")
+        self.feature_scale = feature_scale
+        self.use_first_pool = use_first_pool
+        self.model = resnet34_trunk(pretrained, _norm_layer(norm_type))
+        self.latent_size = [0, 64, 128, 256, 512, 1024][num_layers]
+        self.num_layers = num_layers
+        self.index_interp = index_interp
+        self.index_padding = index_padding
+        self.upsample_interp = upsample_interp
+        self.register_buffer("latent", torch.empty(1, 1, 1, 1), persistent=False)
+        self.register_buffer("latent_scaling", torch.empty(2, dtype=torch.float32), persistent=False)
+        # channels-last copy (NS, H_l, W_l, C) read by the HIP gather; a buffer so that
+        # nn.DataParallel replicas get their own device copy
+        self.register_buffer("latent_cl", torch.empty(0), persistent=False)
+
+    def set_latent(self, latent):
+        """Install a feature map (NS, C, H_l, W_l) as forward() would (encoder.py:160-163)."""
+        self.latent = latent
+        ls = torch.tensor([latent.shape[-1], latent.shape[-2]], dtype=torch.float32,
+                          device=latent.device)
+        self.latent_scaling = ls / (ls - 1) * 2.0
+        self.latent_cl = latent.permute(0, 2, 3, 1).contiguous()
+        return latent
+
+    def forward(self, x):
+        if self.feature_scale != 1.0:
+            x = F.interpolate(x, scale_factor=self.feature_scale,
+                              mode="bilinear" if self.feature_scale > 1.0 else "area",
+                              align_corners=True if self.feature_scale > 1.0 else None,
+                              recompute_scale_factor=True)
+        x = x.to(device=self.latent.device)
+        m = self.model
+        x = m.relu(m.bn1(m.conv1(x)))
+        latents = [x]
+        if self.num_layers > 1:
+            if self.use_first_pool:
+                x = m.maxpool(x)
+            x = m.layer1(x)
+            latents.append(x)
+        if self.num_layers > 2:
+            x = m.layer2(x)
+            latents.append(x)
+        if self.num_layers > 3:
+            x = m.layer3(x)
+            latents.append(x)
+        if self.num_layers > 4:
+            x = m.layer4(x)
+            latents.append(x)
+        size = latents[0].shape[-2:]
+        for i in range(len(latents)):
+            latents[i] = F.interpolate(latents[i], size, mode=self.upsample_interp,
+                                       align_corners=True)
+        return self.set_latent(torch.cat(latents, dim=1))
+
+    def index(self, uv, cam_z=None, image_size=(), z_bounds=None):
+        """Bilinear feature lookup at image points (encoder.py:80-109); utility only —
+        the ray march does this gather inside the fused HIP kernel."""
+        if uv.shape[0] == 1 and self.latent.shape[0] > 1:
+            uv = uv.expand(self.latent.shape[0], -1, -1)
+        if len(image_size) > 0:
+            if len(image_size) == 1:
+                image_size = (image_size, image_size)
+            scale = self.latent_scaling / image_size
+            uv = uv * scale - 1.0
+        samples = F.grid_sample(self.latent, uv.unsqueeze(2), align_corners=True,
+                                mode=self.index_interp, padding_mode=self.index_padding)
+        return samples[:, :, :, 0]
+
+    @classmethod
+    def from_conf(cls, conf):
+        return cls(conf.get_string("backbone"), pretrained=conf.get_bool("pretrained", True),
+                   num_layers=conf.get_int("num_layers", 4),
+                   index_interp=conf.get_string("index_interp", "bilinear"),
+                   index_padding=conf.get_string("index_padding", "border"),
+                   upsample_interp=conf.get_string("upsample_interp", "bilinear"),
+                   feature_scale=conf.get_float("feature_scale", 1.0),
+                   use_first_pool=conf.get_bool("use_first_pool", True))

@@ -1,0 +1,404 @@
+"""PixelNeRFNet / ResnetFC / PositionalEncoding with the reference's interface.
+
+Same constructor (``make_model(conf)``), ``encode``, ``forward``,
+``load_weights`` / ``save_weights``, buffers and state-dict keys as the reference
+(models.py:15-316, resnetfc.py:10-198, code.py:6-52) so checkpoints load
+unchanged.  The per-point evaluation (``forward``, models.py:146-266) and the
+full ray march (``pnr.renderer.NeRFRenderer``) run in libpnr.so on the HIP
+device; the nn.Linear modules here are the parameter store the kernels read
+(packed once per weight version by ``pnr_mlp_pack``).
+"""
+import os
+import os.path as osp
+import warnings
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from .conf import as_conf
+from .encoder import SpatialEncoder
+
+__all__ = ["PositionalEncoding", "ResnetBlockFC", "ResnetFC", "PixelNeRFNet", "make_model",
+           "make_mlp", "make_encoder"]
+
+
+class PositionalEncoding(nn.Module):
+    """NeRF sin/cos encoding (code.py:6-52); cos computed as sin(x + pi/2)."""
+
+    def __init__(self, num_freqs=6, d_in=3, freq_factor=np.pi, include_input=True):
+        super().__init__()
+        self.num_freqs = num_freqs
+        self.d_in = d_in
+        self.freqs = freq_factor * 2.0 ** torch.arange(0, num_freqs)
+        self.d_out = self.num_freqs * 2 * d_in + (d_in if include_input else 0)
+        self.include_input = include_input
+        self.register_buffer("_freqs", torch.repeat_interleave(self.freqs, 2).view(1, -1, 1))
+        phases = torch.zeros(2 * self.num_freqs)
+        phases[1::2] = np.pi * 0.5
+        self.register_buffer("_phases", phases.view(1, -1, 1))
+
+    def forward(self, x):
+        embed = x.unsqueeze(1).repeat(1, self.num_freqs * 2, 1)
+        embed = torch.sin(torch.addcmul(self._phases, embed, self._freqs))
+        embed = embed.view(x.shape[0], -1)
+        return torch.cat((x, embed), dim=-1) if self.include_input else embed
+
+    @classmethod
+    def from_conf(cls, conf, d_in=3):
+        return cls(conf.get_int("num_freqs", 6), d_in, conf.get_float("freq_factor", np.pi),
+                   conf.get_bool("include_input", True))
+
+
+class ResnetBlockFC(nn.Module):
+    """x + fc_1(relu(fc_0(relu(x)))) (resnetfc.py:10-62); parameters only."""
+
+    def __init__(self, size_in, size_out=None, size_h=None, beta=0.0):
+        super().__init__()
+        size_out = size_in if size_out is None else size_out
+        size_h = min(size_in, size_out) if size_h is None else size_h
+        self.size_in, self.size_h, self.size_out = size_in, size_h, size_out
+        self.fc_0 = nn.Linear(size_in, size_h)
+        self.fc_1 = nn.Linear(size_h, size_out)
+        nn.init.constant_(self.fc_0.bias, 0.0)
+        nn.init.kaiming_normal_(self.fc_0.weight, a=0, mode="fan_in")
+        nn.init.constant_(self.fc_1.bias, 0.0)
+        nn.init.zeros_(self.fc_1.weight)
+        self.beta = beta
+        self.shortcut = None
+        if size_in != size_out:
+            self.shortcut = nn.Linear(size_in, size_out, bias=False)
+
+
+class ResnetFC(nn.Module):
+    """ResnetFC parameter layout (resnetfc.py:65-198)."""
+
+    def __init__(self, d_in, d_out=4, n_blocks=5, d_latent=0, d_hidden=128, beta=0.0,
+                 combine_layer=1000, combine_type="average", use_spade=False):
+        super().__init__()
+        if d_in > 0:
+            self.lin_in = nn.Linear(d_in, d_hidden)
+            nn.init.constant_(self.lin_in.bias, 0.0)
+            nn.init.kaiming_normal_(self.lin_in.weight, a=0, mode="fan_in")
+        self.lin_out = nn.Linear(d_hidden, d_out)
+        nn.init.constant_(self.lin_out.bias, 0.0)
+        nn.init.kaiming_normal_(self.lin_out.weight, a=0, mode="fan_in")
+        self.n_blocks, self.d_latent, self.d_in = n_blocks, d_latent, d_in
+        self.d_out, self.d_hidden = d_out, d_hidden
+        self.combine_layer, self.combine_type, self.use_spade = combine_layer, combine_type, use_spade
+        self.beta = beta
+        self.blocks = nn.ModuleList([ResnetBlockFC(d_hidden, beta=beta) for _ in range(n_blocks)])
+        if d_latent != 0:
+            n_lin_z = min(combine_layer, n_blocks)
+            self.lin_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
+            for lz in self.lin_z:
+                nn.init.constant_(lz.bias, 0.0)
+                nn.init.kaiming_normal_(lz.weight, a=0, mode="fan_in")
+            if use_spade:
+                self.scale_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
+
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("ResnetFC is evaluated inside the fused HIP kernel; call "
+                                  "PixelNeRFNet.forward or NeRFRenderer instead")
+
+    @classmethod
+    def from_conf(cls, conf, d_in, **kwargs):
+        return cls(d_in, n_blocks=conf.get_int("n_blocks", 5), d_hidden=conf.get_int("d_hidden", 128),
+                   beta=conf.get_float("beta", 0.0), combine_layer=conf.get_int("combine_layer", 1000),
+                   combine_type=conf.get_string("combine_type", "average"),
+                   use_spade=conf.get_bool("use_spade", False), **kwargs)
+
+    # ---- HIP packing -----------------------------------------------------------------
+    def hip_unsupported_reason(self):
+        if self.d_in <= 0 or self.d_latent != 512 or self.d_hidden != 512:
+            return "d_hidden = d_latent = 512 and d_in > 0 required (got %d/%d/%d)" % (
+                self.d_hidden, self.d_latent, self.d_in)
+        if self.d_out != 4:
+            return "d_out must be 4"
+        if self.beta > 0:
+            return "softplus activation (beta > 0) not implemented"
+        if self.combine_type != "average":
+            return "combine_type %r not implemented" % self.combine_type
+        if self.use_spade:
+            return "use_spade not implemented"
+        if self.n_blocks > 8:
+            return "n_blocks > 8"
+        return None
+
+    def desc(self, pe_n):
+        return _lib.MlpDesc(self.d_in, self.d_latent, self.d_hidden, self.d_out, self.n_blocks,
+                            self.combine_layer, pe_n)
+
+    def packed(self, code):
+        """Packed fragment-order copy of the weights (re-packed when they change)."""
+        params = [p for p in self.parameters()] + [code._freqs, code._phases]
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        cache = self.__dict__.get("_pnr_pack")
+        if cache is not None and cache[0] == key:
+            return cache[1], cache[2]
+        pe_n = int(code._freqs.numel())
+        desc = self.desc(pe_n)
+        lib = _lib.load()
+        nbytes = lib.pnr_mlp_packed_bytes(desc)
+        if nbytes == 0:
+            _lib.check(-2, "pnr_mlp_packed_bytes")
+        dev = self.lin_out.weight.device
+        buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        keep = []
+
+        def p(t):
+            t = t.detach().float().contiguous()
+            keep.append(t)
+            return t.data_ptr()
+
+        w = _lib.MlpWeights()
+        w.desc = desc
+        w.lin_in_w, w.lin_in_b = p(self.lin_in.weight), p(self.lin_in.bias)
+        w.lin_out_w, w.lin_out_b = p(self.lin_out.weight), p(self.lin_out.bias)
+        for i, lz in enumerate(getattr(self, "lin_z", [])):
+            w.lin_z_w[i], w.lin_z_b[i] = p(lz.weight), p(lz.bias)
+        for i, blk in enumerate(self.blocks):
+            w.fc0_w[i], w.fc0_b[i] = p(blk.fc_0.weight), p(blk.fc_0.bias)
+            w.fc1_w[i], w.fc1_b[i] = p(blk.fc_1.weight), p(blk.fc_1.bias)
+        w.pe_freqs, w.pe_phases = p(code._freqs.reshape(-1)), p(code._phases.reshape(-1))
+        _lib.check(lib.pnr_mlp_pack(w, _lib.ptr(buf), nbytes, _lib.stream_of(dev)), "pnr_mlp_pack")
+        torch.cuda.current_stream(dev).synchronize()  # `keep` temporaries may be freed after
+        self.__dict__["_pnr_pack"] = (key, desc, buf)
+        return desc, buf
+
+
+def make_mlp(conf, d_in, d_latent=0, allow_empty=False, **kwargs):
+    """model_util.py:5-15 (type = resnet is the implemented MLP)."""
+    mlp_type = conf.get_string("type", "mlp")
+    if mlp_type == "resnet":
+        return ResnetFC.from_conf(conf, d_in, d_latent=d_latent, **kwargs)
+    if mlp_type == "empty" and allow_empty:
+        return None
+    raise NotImplementedError("Unsupported MLP type %r (pnr implements type = resnet)" % mlp_type)
+
+
+def make_encoder(conf, **kwargs):
+    enc_type = conf.get_string("type", "spatial")
+    if enc_type == "spatial":
+        return SpatialEncoder.from_conf(conf, **kwargs)
+    raise NotImplementedError("Unsupported encoder type %r" % enc_type)
+
+
+class PixelNeRFNet(nn.Module):
+    """pixelNeRF network (models.py:15-316)."""
+
+    def __init__(self, conf, stop_encoder_grad=False):
+        super().__init__()
+        conf = as_conf(conf)
+        self.encoder = make_encoder(conf["encoder"])
+        self.use_encoder = conf.get_bool("use_encoder", True)
+        self.use_xyz = conf.get_bool("use_xyz", False)
+        assert self.use_encoder or self.use_xyz
+        self.normalize_z = conf.get_bool("normalize_z", True)
+        self.stop_encoder_grad = stop_encoder_grad
+        self.use_code = conf.get_bool("use_code", False)
+        self.use_code_viewdirs = conf.get_bool("use_code_viewdirs", True)
+        self.use_viewdirs = conf.get_bool("use_viewdirs", False)
+        self.use_global_encoder = conf.get_bool("use_global_encoder", False)
+        d_latent = self.encoder.latent_size if self.use_encoder else 0
+        d_in = 3 if self.use_xyz else 1
+        if self.use_viewdirs and self.use_code_viewdirs:
+            d_in += 3
+        self.code = None
+        if self.use_code and d_in > 0:
+            self.code = PositionalEncoding.from_conf(conf["code"], d_in=d_in)
+            d_in = self.code.d_out
+        if self.use_viewdirs and not self.use_code_viewdirs:
+            d_in += 3
+        if self.use_global_encoder:
+            raise NotImplementedError("use_global_encoder is not implemented by the HIP path")
+        d_out = 4
+        self.latent_size = self.encoder.latent_size
+        self.mlp_coarse = make_mlp(conf["mlp_coarse"], d_in, d_latent, d_out=d_out)
+        self.mlp_fine = make_mlp(conf["mlp_fine"], d_in, d_latent, d_out=d_out, allow_empty=True)
+        self.register_buffer("poses", torch.empty(1, 3, 4), persistent=False)
+        self.register_buffer("image_shape", torch.empty(2), persistent=False)
+        self.d_in, self.d_out, self.d_latent = d_in, d_out, d_latent
+        self.register_buffer("focal", torch.empty(1, 2), persistent=False)
+        self.register_buffer("c", torch.empty(1, 2), persistent=False)
+        # HIP-side scene: per-(object, view) camera records (SB*NS, 16)
+        self.register_buffer("cams", torch.empty(0, 16), persistent=False)
+        self.num_objs = 0
+        self.num_views_per_obj = 1
+
+    # ---- encode ---------------------------------------------------------------------
+    def encode(self, images, poses, focal, z_bounds=None, c=None):
+        """models.py:89-144: run the encoder CNN, then set world->camera poses and
+        intrinsics.  images (NS, 3, H, W) or (SB, NS, 3, H, W)."""
+        self.num_objs = images.size(0)
+        if len(images.shape) == 5:
+            assert len(poses.shape) == 4 and poses.size(1) == images.size(1)
+            self.num_views_per_obj = images.size(1)
+            images = images.reshape(-1, *images.shape[2:])
+            poses = poses.reshape(-1, 4, 4)
+        else:
+            self.num_views_per_obj = 1
+        self.encoder(images)
+        self._set_cameras(poses, focal, c, images.shape[-1], images.shape[-2])
+
+    def encode_latent(self, latent, poses, focal, image_size, c=None, num_objs=1):
+        """Install a precomputed feature map (SB*NS, C, H_l, W_l) instead of running the
+        CNN; ``image_size`` = (W, H) of the source images."""
+        ns = latent.shape[0] // num_objs
+        self.num_objs = num_objs
+        self.num_views_per_obj = ns
+        if poses.dim() == 4:
+            poses = poses.reshape(-1, 4, 4)
+        self.encoder.set_latent(latent.float().contiguous())
+        self._set_cameras(poses, focal, c, image_size[0], image_size[1])
+
+    def _set_cameras(self, poses, focal, c, width, height):
+        dev = self.encoder.latent.device
+        poses = poses.to(dev).float()
+        rot = poses[:, :3, :3].transpose(1, 2)
+        trans = -torch.bmm(rot, poses[:, :3, 3:])
+        self.poses = torch.cat((rot, trans), dim=-1)
+        self.image_shape = torch.tensor([float(width), float(height)], device=dev)
+        focal = torch.as_tensor(focal).to(dev)
+        if focal.dim() == 0:
+            focal = focal[None, None].repeat((1, 2))
+        elif focal.dim() == 1:
+            focal = focal.unsqueeze(-1).repeat((1, 2))
+        else:
+            focal = focal.clone()
+        self.focal = focal.float()
+        self.focal[..., 1] *= -1.0
+        if c is None:
+            c = (self.image_shape * 0.5).unsqueeze(0)
+        else:
+            c = torch.as_tensor(c).to(dev).float()
+            if c.dim() == 0:
+                c = c[None, None].repeat((1, 2))
+            elif c.dim() == 1:
+                c = c.unsqueeze(-1).repeat((1, 2))
+        self.c = c
+        self._build_cams()
+
+    def _build_cams(self):
+        sb, ns = self.num_objs, self.num_views_per_obj
+        n = self.poses.shape[0]
+        if n != sb * ns:
+            raise ValueError("poses (%d) != objects (%d) x views (%d)" % (n, sb, ns))
+        obj = torch.arange(n, device=self.poses.device) // ns
+
+        def per_obj(t, name):
+            if t.shape[0] == 1:
+                return t.expand(n, 2)
+            if t.shape[0] == sb:
+                return t[obj]
+            raise ValueError("%s has %d rows; expected 1 or %d (one per object)" % (name, t.shape[0], sb))
+
+        f = per_obj(self.focal, "focal")
+        c = per_obj(self.c, "c")
+        self.cams = torch.cat([self.poses[:, :, :3].reshape(n, 9), self.poses[:, :, 3], f, c],
+                              dim=1).float().contiguous()
+
+    # ---- HIP scene ------------------------------------------------------------------
+    def hip_unsupported_reason(self):
+        if not (self.use_encoder and self.use_xyz and self.normalize_z and self.use_code
+                and self.use_viewdirs and not self.use_code_viewdirs):
+            return ("the fused kernel implements use_encoder, use_xyz, normalize_z, use_code, "
+                    "use_viewdirs with use_code_viewdirs = False (the shipped confs)")
+        if self.code is None or not self.code.include_input:
+            return "positional encoding must include the input"
+        for mlp in (self.mlp_coarse, self.mlp_fine):
+            if mlp is not None:
+                r = mlp.hip_unsupported_reason()
+                if r:
+                    return r
+        if self.encoder.latent_cl.numel() == 0:
+            return "encode() has not been called"
+        if self.num_views_per_obj > 1 and self.mlp_coarse.combine_layer >= self.mlp_coarse.n_blocks:
+            return "multi-view input needs combine_layer < n_blocks"
+        return None
+
+    def _require_hip(self):
+        r = self.hip_unsupported_reason()
+        if r:
+            raise NotImplementedError("pnr: " + r)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "pnr: the HIP ray march is forward-only (training backward is SURVEY §8(f) "
+                "rank 2); run under torch.no_grad() or freeze the parameters")
+
+    def hip_scene(self):
+        lat = self.encoder.latent_cl
+        sc = _lib.Scene()
+        sc.latent = lat.data_ptr()
+        sc.cams = self.cams.data_ptr()
+        sc.n_obj = self.num_objs
+        sc.n_views = self.num_views_per_obj
+        sc.latent_h, sc.latent_w, sc.latent_c = lat.shape[1], lat.shape[2], lat.shape[3]
+        sc.image_w, sc.image_h = float(self.image_shape[0]), float(self.image_shape[1])
+        return sc
+
+    def hip_mlp(self, coarse):
+        mlp = self.mlp_coarse if (coarse or self.mlp_fine is None) else self.mlp_fine
+        return mlp.packed(self.code)
+
+    # ---- forward (point query) -----------------------------------------------------
+    def forward(self, xyz, coarse=True, viewdirs=None, far=False):
+        """(SB, B, 3) world points -> (SB, B, 4) [sigmoid(rgb), relu(sigma)]
+        (models.py:146-266) on the HIP device."""
+        self._require_hip()
+        SB, B, _ = xyz.shape
+        if SB != self.num_objs:
+            raise ValueError("xyz has %d objects but encode() saw %d" % (SB, self.num_objs))
+        from .ops import _dev
+
+        xyz = _dev(xyz, "xyz")
+        vd = _dev(viewdirs.reshape(SB, B, 3), "viewdirs") if viewdirs is not None else None
+        desc, packed = self.hip_mlp(coarse)
+        sc = self.hip_scene()
+        lib = _lib.load()
+        ws_bytes = lib.pnr_point_query_workspace_bytes(sc, SB * B)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xyz.device)
+        out = torch.empty(SB, B, 4, dtype=torch.float32, device=xyz.device)
+        _lib.check(lib.pnr_point_query(sc, desc, _lib.ptr(packed), _lib.ptr(xyz), _lib.ptr(vd), B,
+                                       _lib.ptr(out), _lib.ptr(ws), ws_bytes,
+                                       _lib.stream_of(xyz.device)), "pnr_point_query")
+        return out
+
+    # ---- checkpoints (models.py:268-316) -------------------------------------------
+    def load_weights(self, args, opt_init=False, strict=True, device=None):
+        if opt_init and not args.resume:
+            return
+        ckpt_name = "pixel_nerf_init" if opt_init or not args.resume else "pixel_nerf_latest"
+        model_path = "%s/%s/%s" % (args.checkpoints_path, args.name, ckpt_name)
+        if device is None:
+            device = self.poses.device
+        if os.path.exists(model_path):
+            print("Load", model_path)
+            self.load_state_dict(torch.load(model_path, map_location=device, weights_only=True),
+                                 strict=strict)
+        elif not opt_init:
+            warnings.warn("WARNING: {} does not exist, not loaded!! Model will be "
+                          "re-initialized.".format(model_path))
+        return self
+
+    def save_weights(self, args, opt_init=False):
+        from shutil import copyfile
+
+        ckpt_name = "pixel_nerf_init" if opt_init else "pixel_nerf_latest"
+        backup_name = "pixel_nerf_init_backup" if opt_init else "pixel_nerf_backup"
+        ckpt_path = osp.join(args.checkpoints_path, args.name, ckpt_name)
+        ckpt_backup_path = osp.join(args.checkpoints_path, args.name, backup_name)
+        if osp.exists(ckpt_path):
+            copyfile(ckpt_path, ckpt_backup_path)
+        torch.save(self.state_dict(), ckpt_path)
+        return self
+
+
+def make_model(conf, *args, **kwargs):
+    """model/__init__.py:4-11."""
+    conf = as_conf(conf)
+    model_type = conf.get_string("type", "pixelnerf")
+    if model_type == "pixelnerf":
+        return PixelNeRFNet(conf, *args, **kwargs)
+    raise NotImplementedError("Unsupported model type", model_type)

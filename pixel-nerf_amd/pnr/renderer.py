@@ -1,0 +1,243 @@
+"""NeRFRenderer with the reference's interface (src/render/nerf.py:15-371).
+
+``NeRFRenderer.forward(model, rays, want_weights)`` keeps the reference's
+contract.  When ``model`` is a :class:`pnr.models.PixelNeRFNet` the whole coarse
++ fine march (sampling, fused point MLP, compositing, inverse-CDF resampling)
+runs as one stream-ordered sequence in libpnr.so (``pnr_render_forward``).  Any
+other model goes through the reference's plug point ``model(points, coarse,
+viewdirs)`` with sampling and compositing still on the HIP kernels.
+
+Random draws keep the reference's order and shapes on the rays' device
+(nerf.py:111, 135, 141, 158): with the same torch seed this renderer consumes
+the generator exactly as the reference does.
+"""
+import torch
+
+from . import _lib, ops
+from .conf import as_conf
+
+__all__ = ["NeRFRenderer", "DotMap"]
+
+
+class DotMap(dict):
+    """Attribute-access dict with ``toDict`` (the reference returns dotmap.DotMap)."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k)
+
+    def __setattr__(self, k, v):
+        self[k] = v
+
+    def toDict(self):
+        return {k: (v.toDict() if isinstance(v, DotMap) else v) for k, v in self.items()}
+
+
+class _RenderWrapper(torch.nn.Module):
+    """nerf.py:15-42."""
+
+    def __init__(self, net, renderer, simple_output):
+        super().__init__()
+        self.net = net
+        self.renderer = renderer
+        self.simple_output = simple_output
+
+    def forward(self, rays, want_weights=False):
+        if rays.shape[0] == 0:
+            return (torch.zeros(0, 3, device=rays.device), torch.zeros(0, device=rays.device))
+        outputs = self.renderer(self.net, rays, want_weights=want_weights and not self.simple_output)
+        if self.simple_output:
+            part = outputs.fine if self.renderer.using_fine else outputs.coarse
+            return part.rgb, part.depth
+        return outputs.toDict()
+
+
+class NeRFRenderer(torch.nn.Module):
+    """NeRF volume renderer (nerf.py:45-371)."""
+
+    def __init__(self, n_coarse=128, n_fine=0, n_fine_depth=0, noise_std=0.0, depth_std=0.01,
+                 eval_batch_size=100000, white_bkgd=False, lindisp=False, sched=None):
+        super().__init__()
+        self.n_coarse = n_coarse
+        self.n_fine = n_fine
+        self.n_fine_depth = n_fine_depth
+        self.noise_std = noise_std
+        self.depth_std = depth_std
+        self.eval_batch_size = eval_batch_size
+        self.white_bkgd = white_bkgd
+        self.lindisp = lindisp
+        if lindisp:
+            print("Using linear displacement rays")
+        self.using_fine = n_fine > 0
+        self.sched = sched
+        if sched is not None and len(sched) == 0:
+            self.sched = None
+        self.register_buffer("iter_idx", torch.tensor(0, dtype=torch.long), persistent=True)
+        self.register_buffer("last_sched", torch.tensor(0, dtype=torch.long), persistent=True)
+        # test / benchmark hook: explicit (u_coarse, u_fine, u_fine_jit, n_depth)
+        self.streams = None
+
+    # ---- random streams (nerf.py:111, 135, 141, 158) ---------------------------------
+    def draw_streams(self, n_rays, device):
+        if self.streams is not None:
+            s = tuple(t.to(device=device, dtype=torch.float32).contiguous() for t in self.streams)
+            self.streams = None
+            return s
+        nf = self.n_fine - self.n_fine_depth
+        u_c = torch.rand(n_rays, self.n_coarse, device=device)
+        empty = torch.zeros(n_rays, 0, device=device)
+        u_f = u_j = n_d = empty
+        if self.using_fine:
+            if nf > 0:
+                u_f = torch.rand(n_rays, nf, device=device)
+                u_j = torch.rand(n_rays, nf, device=device)
+            if self.n_fine_depth > 0:
+                n_d = torch.randn(n_rays, self.n_fine_depth, device=device)
+        return u_c, u_f, u_j, n_d
+
+    # ---- building blocks (HIP) -------------------------------------------------------
+    def sample_coarse(self, rays, u=None):
+        if u is None:
+            u = torch.rand(rays.shape[0], self.n_coarse, device=rays.device)
+        return ops.sample_coarse(rays, self.n_coarse, u, self.lindisp)
+
+    def composite(self, model, rays, z_samp, coarse=True, sb=0):
+        """nerf.py:163-249 through the model callback; compositing on the HIP kernel."""
+        B, K = z_samp.shape
+        points = rays[:, None, :3] + z_samp.unsqueeze(2) * rays[:, None, 3:6]
+        points = points.reshape(-1, 3)
+        use_viewdirs = hasattr(model, "use_viewdirs") and model.use_viewdirs
+        if sb > 0:
+            points = points.reshape(sb, -1, 3)
+            ebs = (self.eval_batch_size - 1) // sb + 1
+            dim = 1
+        else:
+            ebs, dim = self.eval_batch_size, 0
+        vals = []
+        if use_viewdirs:
+            vd = rays[:, None, 3:6].expand(-1, K, -1)
+            vd = vd.reshape(sb, -1, 3) if sb > 0 else vd.reshape(-1, 3)
+            for pts, dirs in zip(torch.split(points, ebs, dim=dim), torch.split(vd, ebs, dim=dim)):
+                vals.append(model(pts, coarse=coarse, viewdirs=dirs))
+        else:
+            for pts in torch.split(points, ebs, dim=dim):
+                vals.append(model(pts, coarse=coarse))
+        out = torch.cat(vals, dim=dim).reshape(B, K, -1)
+        if self.training and self.noise_std > 0.0:
+            out = out.clone()
+            out[..., 3] = out[..., 3] + torch.randn_like(out[..., 3]) * self.noise_std
+        return ops.composite(z_samp, out[..., :4].contiguous(), rays, self.white_bkgd)
+
+    # ---- forward (nerf.py:251-303) ---------------------------------------------------
+    def forward(self, model, rays, want_weights=False):
+        if self.sched is not None and self.last_sched.item() > 0:
+            self.n_coarse = self.sched[1][self.last_sched.item() - 1]
+            self.n_fine = self.sched[2][self.last_sched.item() - 1]
+        assert len(rays.shape) == 3
+        sb = rays.shape[0]
+        rays = rays.reshape(-1, 8).contiguous()
+        B = rays.shape[0]
+        if self.using_fine and self.n_fine <= 0:
+            raise NotImplementedError("using_fine with n_fine = 0 (fine pass over coarse samples only)")
+        streams = self.draw_streams(B, rays.device)
+        from .models import PixelNeRFNet
+
+        if isinstance(model, PixelNeRFNet):
+            return self._forward_fused(model, rays, sb, streams, want_weights)
+        return self._forward_callback(model, rays, sb, streams, want_weights)
+
+    def _pack_out(self, w, rgb, depth, sb, want_weights):
+        d = DotMap(rgb=rgb.reshape(sb, -1, 3), depth=depth.reshape(sb, -1))
+        if want_weights:
+            d.weights = w.reshape(sb, -1, w.shape[-1])
+        return d
+
+    def _forward_fused(self, net, rays, sb, streams, want_weights):
+        net._require_hip()
+        if rays.device.type != "cuda":
+            raise ValueError("pnr: rays must be on the HIP device")
+        if self.training and self.noise_std > 0.0:
+            raise NotImplementedError("noise_std > 0 in training mode is not implemented")
+        B = rays.shape[0]
+        dev = rays.device
+        kc, kf = self.n_coarse, (self.n_fine if self.using_fine else 0)
+        kfd = self.n_fine_depth if self.using_fine else 0
+        u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
+        cfg = _lib.RenderCfg(kc, kf, kfd, float(self.depth_std), int(bool(self.white_bkgd)),
+                             int(bool(self.lindisp)))
+        sc = net.hip_scene()
+        desc, pc = net.hip_mlp(True)
+        _, pf = net.hip_mlp(False) if kf > 0 else (None, None)
+        f32 = dict(device=dev, dtype=torch.float32)
+        c_rgb, c_depth = torch.empty(B, 3, **f32), torch.empty(B, **f32)
+        c_w = torch.empty(B, kc, **f32) if want_weights or kf > 0 else None
+        f_rgb = torch.empty(B, 3, **f32) if kf > 0 else None
+        f_depth = torch.empty(B, **f32) if kf > 0 else None
+        f_w = torch.empty(B, kc + kf, **f32) if (want_weights and kf > 0) else None
+        out = _lib.RenderOut(c_rgb.data_ptr(), c_depth.data_ptr(),
+                             c_w.data_ptr() if c_w is not None else None,
+                             f_rgb.data_ptr() if f_rgb is not None else None,
+                             f_depth.data_ptr() if f_depth is not None else None,
+                             f_w.data_ptr() if f_w is not None else None, None, None)
+        r = _lib.Rays(rays.data_ptr(), B, B // sb)
+        rng = _lib.Rng(u_c.data_ptr(), u_f.data_ptr() if u_f.numel() else None,
+                       u_j.data_ptr() if u_j.numel() else None,
+                       n_d.data_ptr() if n_d.numel() else None)
+        lib = _lib.load()
+        ws_bytes = lib.pnr_render_workspace_bytes(sc, cfg, B)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        _lib.check(lib.pnr_render_forward(sc, desc, _lib.ptr(pc), _lib.ptr(pf) if pf is not None else None,
+                                          r, rng, cfg, out, _lib.ptr(ws), ws_bytes,
+                                          _lib.stream_of(dev)), "pnr_render_forward")
+        outputs = DotMap(coarse=self._pack_out(c_w, c_rgb, c_depth, sb, want_weights))
+        if kf > 0:
+            outputs.fine = self._pack_out(f_w, f_rgb, f_depth, sb, want_weights)
+        return outputs
+
+    def _forward_callback(self, model, rays, sb, streams, want_weights):
+        u_c, u_f, u_j, n_d = streams
+        z_c = self.sample_coarse(rays, u_c)
+        w_c, rgb_c, depth_c = self.composite(model, rays, z_c, coarse=True, sb=sb)
+        outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, depth_c, sb, want_weights))
+        if self.using_fine:
+            z_f = ops.sample_fine(rays, z_c, w_c.detach(), depth_c, self.n_fine, self.n_fine_depth,
+                                  self.depth_std, u_f, u_j, n_d, self.lindisp)
+            w_f, rgb_f, depth_f = self.composite(model, rays, z_f, coarse=False, sb=sb)
+            outputs.fine = self._pack_out(w_f, rgb_f, depth_f, sb, want_weights)
+        return outputs
+
+    # ---- schedule / construction / parallel (nerf.py:318-371) ------------------------
+    def sched_step(self, steps=1):
+        if self.sched is None:
+            return
+        self.iter_idx += steps
+        while (self.last_sched.item() < len(self.sched[0])
+               and self.iter_idx.item() >= self.sched[0][self.last_sched.item()]):
+            self.n_coarse = self.sched[1][self.last_sched.item()]
+            self.n_fine = self.sched[2][self.last_sched.item()]
+            print("INFO: NeRF sampling resolution changed on schedule ==> c", self.n_coarse,
+                  "f", self.n_fine)
+            self.last_sched += 1
+
+    @classmethod
+    def from_conf(cls, conf, white_bkgd=False, lindisp=False, eval_batch_size=100000):
+        conf = as_conf(conf)
+        return cls(conf.get_int("n_coarse", 128), conf.get_int("n_fine", 0),
+                   n_fine_depth=conf.get_int("n_fine_depth", 0),
+                   noise_std=conf.get_float("noise_std", 0.0),
+                   depth_std=conf.get_float("depth_std", 0.01),
+                   white_bkgd=conf.get_float("white_bkgd", white_bkgd), lindisp=lindisp,
+                   eval_batch_size=conf.get_int("eval_batch_size", eval_batch_size),
+                   sched=conf.get_list("sched", None))
+
+    def bind_parallel(self, net, gpus=None, simple_output=False):
+        """nerf.py:354-371.  With several GPU ids this wraps in nn.DataParallel like the
+        reference; the MI355X-native scaling path is one process per GPU
+        (see pnr.dist / bench.py)."""
+        wrapped = _RenderWrapper(net, self, simple_output=simple_output)
+        if gpus is not None and len(gpus) > 1:
+            print("Using multi-GPU", gpus)
+            wrapped = torch.nn.DataParallel(wrapped, gpus, dim=1)
+        return wrapped

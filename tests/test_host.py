@@ -1,0 +1,162 @@
+"""CPU-only tests: the C-ABI library's exports, host-side API plumbing, config
+parsing, RNG stream order and the no-fallback guarantee."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+import fixtures
+from pnr import _lib, conf, ops, synth
+from pnr.models import PixelNeRFNet, make_model
+from pnr.renderer import DotMap, NeRFRenderer
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "pnr_abi.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pnr_[a-z_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    names = header_functions()
+    assert len(names) >= 12, names
+    lib = ctypes.CDLL(_lib.LIB_PATH)  # loads without a GPU; no compute call is made
+    for n in names:
+        assert hasattr(lib, n), "libpnr.so does not export %s" % n
+    # the Python binding declares exactly the header's functions
+    assert sorted(_lib.SIGNATURES) == names
+
+
+def test_abi_version_and_error_channel():
+    lib = _lib.load()
+    assert lib.pnr_abi_version() == 1
+    # an invalid call fails with a message, without touching the GPU
+    rc = lib.pnr_composite(None, None, None, 4, 0, 0, None, None, None, None)
+    assert rc == -1
+    assert b"bad sizes" in lib.pnr_last_error()
+    assert lib.pnr_mlp_packed_bytes(_lib.MlpDesc(42, 256, 256, 4, 5, 3, 12)) == 0
+    assert b"512" in lib.pnr_last_error()
+    sz = lib.pnr_mlp_packed_bytes(_lib.MlpDesc(42, 512, 512, 4, 5, 3, 12))
+    # 13 K=512 layers + lin_in (4 k-blocks) + lin_out + biases, in bytes
+    assert 13 * 512 * 512 * 4 < sz < 13 * 512 * 512 * 4 + 600000
+
+
+def test_ops_refuse_cpu_tensors():
+    with pytest.raises(ValueError, match="HIP device"):
+        ops.composite(torch.zeros(2, 3), torch.zeros(2, 3, 4), torch.zeros(2, 8), True)
+    with pytest.raises(ValueError, match="HIP device"):
+        ops.sample_coarse(torch.zeros(2, 8), 4, torch.zeros(2, 4))
+
+
+def _conf_dict():
+    mlp = dict(type="resnet", n_blocks=5, d_hidden=512, combine_layer=3, combine_type="average")
+    return dict(use_encoder=True, use_xyz=True, use_code=True,
+                code=dict(num_freqs=6, freq_factor=1.5, include_input=True), use_viewdirs=True,
+                use_code_viewdirs=False, mlp_coarse=mlp, mlp_fine=dict(mlp),
+                encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
+
+
+def test_model_state_dict_matches_reference_layout():
+    net = make_model(_conf_dict())
+    sd = net.state_dict()
+    ours = sorted(k for k in sd if not k.startswith("encoder."))
+    ref = sorted(synth.pixelnerf_state(0).keys())
+    assert ours == ref and len(ours) == 62
+    for k in ref:
+        assert tuple(sd[k].shape) == tuple(synth.pixelnerf_state(0)[k].shape), k
+    assert net.d_in == 42 and net.d_latent == 512
+    # torchvision resnet34 minus fc: 216 encoder tensors
+    assert sum(1 for k in sd if k.startswith("encoder.model.")) == 216
+
+
+def test_encode_builds_camera_records():
+    cfg, arr = fixtures.load("rw_ns3_sb2")
+    net = make_model(_conf_dict())
+    lat = torch.zeros(6, 512, 4, 5)
+    net.encode_latent(lat, arr["poses"], arr["focal"], (cfg["width"], cfg["height"]), c=arr["c"],
+                      num_objs=2)
+    assert net.num_objs == 2 and net.num_views_per_obj == 3
+    cams = net.cams
+    assert cams.shape == (6, 16)
+    # R_wc = R^T, t_wc = -R^T t (models.py:112-114); fy negated (models.py:130)
+    p = arr["poses"].reshape(6, 4, 4)
+    R = p[:, :3, :3].transpose(1, 2)
+    torch.testing.assert_close(cams[:, :9], R.reshape(6, 9))
+    torch.testing.assert_close(cams[:, 9:12], -(R @ p[:, :3, 3:])[..., 0])
+    torch.testing.assert_close(cams[3:, 12:14], torch.tensor([[280.0, -290.0]] * 3))
+    torch.testing.assert_close(cams[:3, 14:16], torch.tensor([[195.0, 152.0]] * 3))
+    assert net.encoder.latent_cl.shape == (6, 4, 5, 512)
+    # the HIP path refuses CPU tensors loudly (no CPU fallback)
+    with torch.no_grad(), pytest.raises(ValueError, match="HIP device"):
+        net(torch.zeros(2, 4, 3), coarse=True, viewdirs=torch.zeros(2, 4, 3))
+
+
+def test_forward_only_guard():
+    net = make_model(_conf_dict())
+    net.encode_latent(torch.zeros(1, 512, 4, 4), synth.srn_poses([0.0]), torch.tensor(50.0), (32, 32))
+    with pytest.raises(NotImplementedError, match="forward-only"):
+        net(torch.zeros(1, 2, 3), coarse=True, viewdirs=torch.zeros(1, 2, 3))
+
+
+def test_renderer_draws_streams_in_reference_order():
+    """Same seed -> the same four streams the fixtures replay (nerf.py:111,135,141,158)."""
+    r = NeRFRenderer(n_coarse=16, n_fine=16, n_fine_depth=8)
+    torch.manual_seed(1)
+    got = r.draw_streams(64, torch.device("cpu"))
+    exp = synth.rng_streams(1, 64, 16, 16, 8)
+    for a, b in zip(got, exp):
+        assert torch.equal(a, b)
+    cfg, arr = fixtures.load("rw_lindisp")   # streams as stored by make_golden.py
+    r2 = NeRFRenderer(n_coarse=cfg["n_coarse"], n_fine=cfg["n_fine"], n_fine_depth=cfg["n_fine_depth"])
+    torch.manual_seed(cfg["rng_seed"])
+    got = r2.draw_streams(arr["rays"].reshape(-1, 8).shape[0], torch.device("cpu"))
+    for a, k in zip(got, ["u_coarse", "u_fine", "u_fine_jit", "n_depth"]):
+        assert torch.equal(a, arr[k]), k
+
+
+def test_renderer_from_conf_and_sched():
+    c = conf.Conf(dict(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True,
+                       sched=[[10, 20], [32, 16], [16, 8]]))
+    r = NeRFRenderer.from_conf(c, lindisp=False, eval_batch_size=5000)
+    assert (r.n_coarse, r.n_fine, r.n_fine_depth, r.using_fine, r.eval_batch_size) == (64, 32, 16, True, 5000)
+    r.sched_step(10)
+    assert (r.n_coarse, r.n_fine) == (32, 16)
+    r.sched_step(15)
+    assert (r.n_coarse, r.n_fine) == (16, 8) and int(r.last_sched) == 2
+    sd = r.state_dict()
+    assert set(sd) == {"iter_idx", "last_sched"}
+
+
+def test_dotmap_todict():
+    d = DotMap(coarse=DotMap(rgb=1), x=2)
+    assert d.coarse.rgb == 1 and d.toDict() == {"coarse": {"rgb": 1}, "x": 2}
+
+
+def test_hocon_subset_parser(tmp_path):
+    (tmp_path / "base.conf").write_text(
+        "# base\nmodel {\n  use_xyz = True\n  code { num_freqs = 6\n freq_factor = 1.5 }\n"
+        "  mlp_coarse { type = resnet  # comment\n n_blocks = 3 }\n}\nrenderer { sched = [] }\n")
+    (tmp_path / "exp.conf").write_text(
+        'include required("base.conf")\nmodel {\n  mlp_coarse { n_blocks = 5, d_hidden = 512 }\n}\n'
+        "renderer.n_coarse = 64\n")
+    c = conf.parse_file(str(tmp_path / "exp.conf"))
+    m = c["model"]
+    assert m.get_bool("use_xyz") is True and m["code"].get_float("freq_factor") == 1.5
+    assert m["mlp_coarse"].get_string("type") == "resnet"
+    assert m["mlp_coarse"].get_int("n_blocks") == 5 and m["mlp_coarse"].get_int("d_hidden") == 512
+    assert c["renderer"].get_int("n_coarse") == 64 and c["renderer"].get_list("sched") == []
+    assert c.get_int("missing", 7) == 7
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/conf"), reason="reference confs absent")
+def test_parser_reads_reference_confs():
+    for name in ("srn", "sn64", "dtu"):
+        c = conf.parse_file("/root/reference/conf/exp/%s.conf" % name)
+        net = PixelNeRFNet(dict(c["model"], encoder=dict(c["model"]["encoder"], pretrained=False)))
+        assert net.d_in == 42 and net.mlp_coarse.n_blocks == 5
+        assert net.hip_unsupported_reason() == "encode() has not been called"
