@@ -38,6 +38,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from pnr import _lib, synth, util  # noqa: E402
+from pnr import dist as pdist  # noqa: E402
 from pnr.models import PixelNeRFNet  # noqa: E402
 from pnr.renderer import NeRFRenderer  # noqa: E402
 
@@ -154,6 +155,24 @@ def composite_roofline(dev, ev):
     return res
 
 
+def pmc_traffic(kernel, pick):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary (rocprofv3
+    counters cannot be read live from inside the process)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")))
+    if not files:
+        return None
+    vals = []
+    for line in open(files[-1]):
+        if line.startswith("#") or line.startswith("kernel,"):
+            continue
+        f = line.strip().split(",")
+        if kernel in f[0]:
+            vals.append(int(f[5]))
+    return pick(vals) if vals else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -164,11 +183,7 @@ def main():
     ap.add_argument("--no-composite", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+    rank, world, local = pdist.init_from_env("nccl")   # RCCL on ROCm; control plane only
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -218,11 +233,7 @@ def main():
         recording["on"] = False
         if world > 1:
             dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = pdist.max_over_ranks(t1 - t0, device=dev)
     assert bool(torch.isfinite(img).all())
 
     # per-kernel durations from the events recorded in the timed region
@@ -259,7 +270,10 @@ def main():
         "roofline": {"kernel": "k_point_mlp (fine pass)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
-                     "traffic": None, "flop_per_launch": flop_fine,
+                     "traffic": pmc_traffic("k_point_mlp", max),
+                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
+                                       "bench (profiles/*/pmc_summary.csv, FETCH x2 gfx950 "
+                                       "correction)", "flop_per_launch": flop_fine,
                      "launch_ms": round(avg["mlp_fine"], 4)},
         "kernel_ms": {n: round(v, 4) for n, v in avg.items()},
     }

@@ -1,0 +1,18 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, short bench.  Stops at the first fault /
+# abort / timeout (exit codes other than 0 or 1).
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+echo "== pytest -m gpu"; date
+timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider -rA > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/gpu_tests.log
+ok $rc || exit $rc
+echo "== smoke"; date
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
+ok $rc || exit $rc
+echo "== bench"; date
+timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-5} --warmup 1 > gpurun_out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
+exit $rc

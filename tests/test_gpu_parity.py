@@ -52,11 +52,11 @@ def model_conf(n_blocks=5, combine_layer=3):
 
 def hip_net(cfg, arr):
     net = PixelNeRFNet(model_conf(cfg.get("n_blocks", 5), cfg.get("combine_layer", 3)))
+    if not cfg.get("with_fine", True):
+        net.mlp_fine = None      # as eval_approx.py:62-63 does
     sd = fixtures.state_dict(cfg)
     missing, unexpected = net.load_state_dict(sd, strict=False)
     assert not unexpected and all(k.startswith("encoder.") for k in missing)
-    if not cfg.get("with_fine", True):
-        net.mlp_fine = None
     net = net.to(DEV).eval()
     lat = fixtures.latent_of(cfg).to(DEV)
     sb = cfg.get("sb", 1)
@@ -137,7 +137,8 @@ def test_sample_fine_matches_oracle(kc, kf, kfd, lindisp):
     depth = 0.5 + 3.0 * torch.rand(B, generator=g)
     nf = kf - kfd
     u = torch.rand(B, nf, generator=g)
-    u[:4, 0] = float(torch.nextafter(torch.tensor(1.0), torch.tensor(0.0)))  # u >= cdf[-1]
+    if nf > 0:
+        u[:4, 0] = float(torch.nextafter(torch.tensor(1.0), torch.tensor(0.0)))  # u >= cdf[-1]
     uj = torch.rand(B, nf, generator=g)
     nd = torch.randn(B, kfd, generator=g)
     samps = [zc]
