@@ -43,6 +43,18 @@ from pnr.models import PixelNeRFNet  # noqa: E402
 from pnr.renderer import NeRFRenderer  # noqa: E402
 
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
+MFMA_BF16_PEAK_TFLOPS = 2500.0 # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
+# fp32-equivalent peak of each ResnetFC arithmetic mode (pnr.models.PRECISIONS): the
+# split modes issue 6 / 9 bf16 MFMA products per fp32 multiply-add
+PEAK_BY_PRECISION = {"fp32": (MFMA_F32_PEAK_TFLOPS, 1), "bf16x6": (MFMA_BF16_PEAK_TFLOPS / 6, 6),
+                     "bf16x9": (MFMA_BF16_PEAK_TFLOPS / 9, 9)}
+ARITHMETIC = {
+    "fp32": "v_mfma_f32_16x16x4_f32 (fp32 products, fp32 accumulate)",
+    "bf16x6": "exact 3-way bf16 split of both fp32 operands, 6 largest products on "
+              "v_mfma_f32_16x16x32_bf16, fp32 accumulate (error at fp32 unit roundoff; "
+              "profiles/r1/precision_study.json)",
+    "bf16x9": "exact 3-way bf16 split, all 9 products (exact), fp32 accumulate",
+}
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOP_PER_POINT_NS1 = 4761600 + 2101248   # NS*4,761,600 + 2,101,248
 KC, KF = 64, 64
@@ -181,6 +193,7 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-composite", action="store_true")
+    ap.add_argument("--precision", default="bf16x6", choices=sorted(PEAK_BY_PRECISION))
     args = ap.parse_args()
 
     rank, world, local = pdist.init_from_env("nccl")   # RCCL on ROCm; control plane only
@@ -188,6 +201,7 @@ def main():
     dev = torch.device("cuda", local)
 
     sd, net, rays = build_scene(dev, rank)
+    net.mlp_precision = args.precision
     renderer = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True,
                             eval_batch_size=CHUNK).to(dev)
     render_par = renderer.bind_parallel(net, [local], simple_output=True).eval()
@@ -247,6 +261,21 @@ def main():
     pts_fine = CHUNK * (KC + KF)
     flop_fine = pts_fine * FLOP_PER_POINT_NS1
     achieved = flop_fine / (avg["mlp_fine"] * 1e-3) / 1e12
+    peak, terms = PEAK_BY_PRECISION[args.precision]
+
+    # same frame with the plain f32-MFMA arithmetic, for comparison (N = 1 only)
+    value_fp32 = None
+    if world == 1 and args.precision != "fp32":
+        net.mlp_precision = "fp32"
+        with torch.no_grad():
+            step()
+            torch.cuda.synchronize(dev)
+            t2 = time.perf_counter()
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize(dev)
+            value_fp32 = round(2 * W * H / (time.perf_counter() - t2), 1)
+        net.mlp_precision = args.precision
 
     rays_total = W * H * args.steps * world
     value = rays_total / elapsed
@@ -262,14 +291,20 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "arithmetic": ARITHMETIC[args.precision],
+        "value_fp32_mfma": value_fp32,
         "data": "synthetic (hash-initialised ResnetFC weights + latent; SRN geometry)",
         "config": {"workload": "cfg2: SRN-cars 128x128 frame, 1 source view, 4096-ray chunks x "
                                "(64 coarse + 64 fine)", "frame": [W, H], "chunk_rays": CHUNK,
                    "n_coarse": KC, "n_fine": KF, "n_views": 1, "rays_per_step_per_gpu": W * H,
                    "parallelism": "rays sharded by frame, 1 process per GPU"},
         "roofline": {"kernel": "k_point_mlp (fine pass)", "bound": "mfma",
-                     "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFLOPS, 4),
+                     "achieved": round(achieved, 2), "peak": round(peak, 1),
+                     "unit": "TFLOP/s (fp32-equivalent: algorithmic FLOP / launch time)",
+                     "frac": round(achieved / peak, 4),
+                     "mfma_issue": {"tflops": round(achieved * terms, 1),
+                                    "peak": MFMA_F32_PEAK_TFLOPS if terms == 1 else MFMA_BF16_PEAK_TFLOPS,
+                                    "products_per_fma": terms},
                      "traffic": pmc_traffic("k_point_mlp", max),
                      "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
                                        "bench (profiles/*/pmc_summary.csv, FETCH x2 gfx950 "

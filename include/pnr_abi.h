@@ -63,7 +63,19 @@ typedef struct pnr_mlp_desc {
     int32_t n_blocks;      /* 5                                                            */
     int32_t combine_layer; /* 3 (>= n_blocks means never combine; requires n_views == 1)  */
     int32_t pe_n;          /* entries of code._freqs / code._phases (2*num_freqs = 12)    */
+    int32_t precision;     /* PNR_PREC_*: arithmetic of the 512-wide layers (see below)  */
 } pnr_mlp_desc;
+
+/* Arithmetic of the ResnetFC GEMMs (fp32 in, fp32 out, fp32 accumulation in all modes):
+ *   PNR_PREC_F32    v_mfma_f32_16x16x4_f32 — fp32 products, fp32 accumulation.
+ *   PNR_PREC_BF16X9 both operands split EXACTLY into three bf16 parts (x = x0+x1+x2),
+ *                   all 9 part-products on v_mfma_f32_16x16x32_bf16: every product exact,
+ *                   only the fp32 accumulation rounds (numerically an fp32 GEMM).
+ *   PNR_PREC_BF16X6 the 6 largest of those products (drops x1*y2, x2*y1, x2*y2, each
+ *                   < 2^-24 |x y|): error at the fp32 unit roundoff. */
+#define PNR_PREC_F32 0
+#define PNR_PREC_BF16X6 6
+#define PNR_PREC_BF16X9 9
 
 /* Unpacked weights in torch nn.Linear layout: weight (out, in), bias (out). */
 typedef struct pnr_mlp_weights {

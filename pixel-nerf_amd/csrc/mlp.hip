@@ -36,9 +36,16 @@ constexpr int LDS_LD = H + 4;      // floats per column in the LDS activation bu
 constexpr int KB_FLOATS = NRT * 256;          // one k-block of a packed layer (32 KB)
 constexpr int LAYER_FLOATS = NKB * KB_FLOATS; // one packed 512x512 layer (1 MB)
 constexpr int HDR = 64;            // header floats: pe freqs [0,16), phases [16,32)
+// split-bf16 modes (PREC 6 / 9): v_mfma_f32_16x16x32_bf16, k-steps of 32
+constexpr int KS32 = H / 32;       // 16 k-steps for K = 512
+constexpr int KS32_IN = 2;         // lin_in (d_in <= 64)
+constexpr int SRT_FLOATS = 768;    // one (k-step, row tile): 3 parts x 64 lanes x 8 bf16
+constexpr int SKS_FLOATS = NRT * SRT_FLOATS;  // one k-step of a packed layer (96 KB)
 
 struct Layout {
+    int prec;                      // 0 = f32 MFMA, 6 / 9 = split-bf16 products
     int n_linz, n_l512, n_blocks, ncomb, d_in, d_out, pe_n;
+    int64_t layer_floats;
     int64_t off_lin_in, off_l512, off_lin_out, off_bias, nbias, total;
 };
 
@@ -51,9 +58,11 @@ inline Layout make_layout(const pnr_mlp_desc &d) {
     L.d_in = d.d_in;
     L.d_out = d.d_out;
     L.pe_n = d.pe_n;
+    L.prec = d.precision;
+    L.layer_floats = L.prec ? (int64_t)KS32 * SKS_FLOATS : (int64_t)LAYER_FLOATS;
     L.off_lin_in = HDR;
-    L.off_l512 = L.off_lin_in + (int64_t)NKB_IN * KB_FLOATS;
-    L.off_lin_out = L.off_l512 + (int64_t)L.n_l512 * LAYER_FLOATS;
+    L.off_l512 = L.off_lin_in + (L.prec ? (int64_t)KS32_IN * SKS_FLOATS : (int64_t)NKB_IN * KB_FLOATS);
+    L.off_lin_out = L.off_l512 + (int64_t)L.n_l512 * L.layer_floats;
     L.off_bias = L.off_lin_out + (int64_t)NKB * 256;
     L.nbias = (int64_t)(1 + L.n_l512) * H + 16;
     L.total = ((L.off_bias + L.nbias + 63) / 64) * 64;
@@ -80,6 +89,8 @@ __global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
     if (i < HDR) {
         if (i < 16 && i < L.pe_n) v = s.pe_f[i];
         else if (i >= 16 && i < 32 && (i - 16) < L.pe_n) v = s.pe_p[i - 16];
+    } else if (i < L.off_lin_out && L.prec) {
+        return;   // written by k_pack_split
     } else if (i < L.off_l512) {
         const int e = (int)(i - L.off_lin_in);
         const int kb = e / KB_FLOATS, rt = (e / 256) % NRT, lane = (e >> 2) & 63, j = e & 3;
@@ -107,6 +118,57 @@ __global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
     out[i] = v;
 }
 
+// Split packer: one thread per (layer, k-step, row tile, lane) -> 8 weights
+// W[16 rt + (lane & 15)][32 ks + 8 (lane >> 4) + j], each split exactly into three
+// bf16 parts w = w0 + w1 + w2 (RNE), stored part-major: [ks][rt][part][lane][8].
+__device__ __forceinline__ unsigned short bf16_rne(float x) {
+    unsigned u = __float_as_uint(x);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float bf16_to_f(unsigned short h) { return __uint_as_float((unsigned)h << 16); }
+
+__global__ void k_pack_split(PackSrc s, Layout L, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n_in = (int64_t)KS32_IN * NRT * 64;
+    const int64_t n_l = (int64_t)KS32 * NRT * 64;
+    if (t >= n_in + L.n_l512 * n_l) return;
+    int layer, ks, rt, lane;
+    float *dst;
+    if (t < n_in) {
+        layer = -1;
+        ks = (int)(t / (NRT * 64)); rt = (int)((t / 64) % NRT); lane = (int)(t % 64);
+        dst = out + L.off_lin_in + (int64_t)ks * SKS_FLOATS + rt * SRT_FLOATS + lane * 4;
+    } else {
+        const int64_t r = t - n_in;
+        layer = (int)(r / n_l);
+        const int64_t e = r % n_l;
+        ks = (int)(e / (NRT * 64)); rt = (int)((e / 64) % NRT); lane = (int)(e % 64);
+        dst = out + L.off_l512 + layer * L.layer_floats + (int64_t)ks * SKS_FLOATS + rt * SRT_FLOATS + lane * 4;
+    }
+    const int row = 16 * rt + (lane & 15);
+    unsigned short p[3][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int col = 32 * ks + 8 * (lane >> 4) + j;
+        float w = 0.f;
+        if (layer < 0) { if (col < L.d_in) w = s.lin_in_w[(int64_t)row * L.d_in + col]; }
+        else w = s.w[layer][(int64_t)row * H + col];
+        const unsigned short h0 = bf16_rne(w);
+        const float r1 = w - bf16_to_f(h0);
+        const unsigned short h1 = bf16_rne(r1);
+        const float r2 = r1 - bf16_to_f(h1);
+        p[0][j] = h0; p[1][j] = h1; p[2][j] = bf16_rne(r2);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        uint4 v;
+        v.x = p[q][0] | ((unsigned)p[q][1] << 16); v.y = p[q][2] | ((unsigned)p[q][3] << 16);
+        v.z = p[q][4] | ((unsigned)p[q][5] << 16); v.w = p[q][6] | ((unsigned)p[q][7] << 16);
+        *reinterpret_cast<uint4 *>(dst + q * 256) = v;
+    }
+}
+
 // ------------------------------------------------------------------------------
 struct Args {
     const float *packed;
@@ -124,7 +186,7 @@ struct Args {
     int ns, hl, wl;
     float img_w, img_h;
     float *out;
-    float *xsum;       // ns > 1: gridDim.x * COLS * H floats
+    float *xsum;       // scratch: gridDim.x x 2 x (COLS * H) floats (x park, multi-view sum)
     int64_t n_tiles;
 };
 
@@ -170,6 +232,122 @@ __device__ __forceinline__ void gemm(Acc &acc, const float *__restrict__ wp, con
     }
 }
 
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef float f8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+typedef unsigned u4 __attribute__((ext_vector_type(4)));
+
+// exact 3-way split x = x0 + x1 + x2 of 8 fp32 values into bf16 (RNE at each step).
+// Per pair: v_cvt_pk_bf16_f32, then the two halves back to fp32 by a shift / mask
+// (11 VALU per pair, no second conversion).
+__device__ __forceinline__ unsigned cvt_pk(float a, float b) {
+    bf2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, bf2);
+    return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 &x1, bf8 &x2) {
+    const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    u4 p0, p1, p2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float a = x[2 * q], b = x[2 * q + 1];
+        const unsigned h = cvt_pk(a, b);
+        const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+        const unsigned m = cvt_pk(ra, rb);
+        const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
+        p0[q] = h;
+        p1[q] = m;
+        p2[q] = cvt_pk(sa, sb);
+    }
+    x0 = __builtin_bit_cast(bf8, p0);
+    x1 = __builtin_bit_cast(bf8, p1);
+    x2 = __builtin_bit_cast(bf8, p2);
+}
+
+// Split-bf16 GEMM: acc[r][c] += sum over the NTERM largest products of the exact
+// 3-way splits of W and IN (6 terms: error ~ fp32 unit roundoff; 9 terms: every
+// product exact, only fp32 accumulation rounds) on v_mfma_f32_16x16x32_bf16.
+//   wp  : packed layer + this wave's first row tile + lane*4 (floats)
+//   inb : LDS buffer at (column cl, k 8g) of this lane
+// Software pipeline: A fragments stream from L2 three row tiles ahead into a
+// 4-deep register ring; the B fragments of k-step ks+1 are read from LDS at the
+// top of ks and split halfway through ks, so the split VALU overlaps the MFMAs.
+template <int NKS, int NTERM>
+__device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ wp, const float *inb) {
+    bf8 ra[4][3];
+    auto loadA = [&](bf8 (&dst)[3], int ks, int r) {
+        const float *src = wp + (int64_t)ks * SKS_FLOATS + r * SRT_FLOATS;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) dst[q] = *reinterpret_cast<const bf8 *>(src + q * 256);
+    };
+    auto loadB = [&](f4 (&dst)[CT][2], int ks) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const float *bp = inb + c * 16 * LDS_LD + 32 * ks;
+            dst[c][0] = *reinterpret_cast<const f4 *>(bp);
+            dst[c][1] = *reinterpret_cast<const f4 *>(bp + 4);
+        }
+    };
+    bf8 b0[CT], b1[CT], b2[CT];
+    {
+        f4 braw[CT][2];
+        loadB(braw, 0);
+#pragma unroll
+        for (int c = 0; c < CT; ++c) split3(braw[c][0], braw[c][1], b0[c], b1[c], b2[c]);
+    }
+    loadA(ra[0], 0, 0);
+    loadA(ra[1], 0, 1);
+    loadA(ra[2], 0, 2);
+#pragma unroll 1
+    for (int ks = 0; ks < NKS; ++ks) {
+        // branch-free: the last k-step re-reads its own fragments instead of testing
+        const int kn = ks + 1 < NKS ? ks + 1 : ks;
+        f4 braw[CT][2];
+        loadB(braw, kn);
+        bf8 n0[CT], n1[CT], n2[CT];
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            const int rn = r + 3;
+            if (rn < RTW) loadA(ra[rn & 3], ks, rn);
+            else loadA(ra[rn & 3], kn, rn - RTW);
+            // keep the prefetch where it is: without the barrier the scheduler sinks
+            // the loads next to their use to save registers and serializes the ring
+            __builtin_amdgcn_sched_barrier(0);
+            const bf8 *a = ra[r & 3];
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+                f4 v = acc[r][c];
+                if (NTERM >= 9) {
+                    v = mfma_bf(a[2], b2[c], v);
+                    v = mfma_bf(a[1], b2[c], v);
+                    v = mfma_bf(a[2], b1[c], v);
+                }
+                v = mfma_bf(a[2], b0[c], v);
+                v = mfma_bf(a[1], b1[c], v);
+                v = mfma_bf(a[0], b2[c], v);
+                v = mfma_bf(a[1], b0[c], v);
+                v = mfma_bf(a[0], b1[c], v);
+                v = mfma_bf(a[0], b0[c], v);
+                acc[r][c] = v;
+            }
+            if (r == 2) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c) split3(braw[c][0], braw[c][1], n0[c], n1[c], n2[c]);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            b0[c] = n0[c];
+            b1[c] = n1[c];
+            b2[c] = n2[c];
+        }
+    }
+}
+
 // acc = bias (per output row) [+ acc]
 __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bias, int wave, int g,
                                          bool accumulate) {
@@ -179,6 +357,21 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
 #pragma unroll
         for (int c = 0; c < CT; ++c) acc[r][c] = accumulate ? acc[r][c] + b : b;
     }
+}
+
+// x parks in scratch while h occupies the accumulator registers (frees 128 regs
+// for the operand pipelines); each (r, c) is one coalesced 1 KB wave store / load
+__device__ __forceinline__ void park(const Acc &acc, float *xp) {
+#pragma unroll
+    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) *reinterpret_cast<f4 *>(xp + (r * CT + c) * 256) = acc[r][c];
+}
+__device__ __forceinline__ void unpark(Acc &acc, const float *xp) {
+#pragma unroll
+    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[r][c] = *reinterpret_cast<const f4 *>(xp + (r * CT + c) * 256);
 }
 
 // IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane)
@@ -194,6 +387,14 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
         }
 }
 
+template <int PREC, int NK>
+__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, int64_t wl_off,
+                                           int64_t ws_off, const float *inb4, const float *inb8) {
+    if constexpr (PREC == 0) gemm<NK>(acc, layer_base + wl_off, inb4);
+    else gemm_split<NK / 2, PREC>(acc, layer_base + ws_off, inb8);
+}
+
+template <int PREC>
 __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
@@ -208,8 +409,10 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
     const float *pe_p = a.packed + 16;   // code._phases
 
     // per-lane fragment bases
-    const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;
-    const float *inb = inbuf + cl * LDS_LD + 4 * g;     // B: column 16c + cl, k 16kb + 4g
+    const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;         // f32 fragments
+    const int64_t ws_off = (int64_t)(RTW * wave) * SRT_FLOATS + lane * 4;  // split fragments
+    const float *inb = inbuf + cl * LDS_LD + 4 * g;     // B (f32): column 16c + cl, k 16kb + 4g
+    const float *inb8 = inbuf + cl * LDS_LD + 8 * g;    // B (split): k 32ks + 8g
     // feature / gather role: thread -> (column col, quarter qt)
     const int col = tid >> 2, qt = tid & 3;
 
@@ -235,7 +438,9 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             else { dx = dy = dz = 0.f; }
             obj = p / a.points_per_obj;
         }
-        float *xs = a.xsum + (int64_t)(blockIdx.x * WAVES + wave) * (RTW * CT * 256) + lane * 4;
+        // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
+        float *xp = a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + lane * 4;
+        float *xs = xp + COLS * H;
 
         for (int v = 0; v < a.ns; ++v) {
             // ---- per (point, view) geometry (this thread's column) ----------------
@@ -304,7 +509,7 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             __syncthreads();   // features visible
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, g, false);
-            gemm<NKB_IN>(x, a.packed + L.off_lin_in + wl_off, inb);
+            layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, wl_off, ws_off, inb, inb8);
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
@@ -323,17 +528,19 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                 }
                 __syncthreads();
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
-                gemm<NKB>(x, a.packed + L.off_l512 + (int64_t)lz * LAYER_FLOATS + wl_off, inb);
+                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, wl_off, ws_off, inb, inb8);
                 __syncthreads();
                 store_relu(x, inbuf, wave, lane);
+                if constexpr (PREC != 0) park(x, xp);
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, g, false);
-                gemm<NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * LAYER_FLOATS + wl_off, inb);
+                layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, wl_off, ws_off, inb, inb8);
                 __syncthreads();
                 store_relu(h, inbuf, wave, lane);
                 __syncthreads();
+                if constexpr (PREC != 0) unpark(x, xp);
                 add_bias(x, bias + (3 + lz) * H, wave, g, true);
-                gemm<NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * LAYER_FLOATS + wl_off, inb);
+                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, wl_off, ws_off, inb, inb8);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -368,14 +575,16 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             __syncthreads();
             store_relu(x, inbuf, wave, lane);
+            if constexpr (PREC != 0) park(x, xp);
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, g, false);
-            gemm<NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * LAYER_FLOATS + wl_off, inb);
+            layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, wl_off, ws_off, inb, inb8);
             __syncthreads();
             store_relu(h, inbuf, wave, lane);
             __syncthreads();
+            if constexpr (PREC != 0) unpark(x, xp);
             add_bias(x, bias + (2 + l0) * H, wave, g, true);
-            gemm<NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * LAYER_FLOATS + wl_off, inb);
+            layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, wl_off, ws_off, inb, inb8);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w -> columns 16w..
         __syncthreads();
@@ -429,6 +638,8 @@ int mlp_check_desc(const pnr_mlp_desc &d) {
     if (d.d_in != 3 + 3 * d.pe_n + 3)
         return fail(PNR_ERR_UNSUPPORTED, "d_in must be 3 + 3*pe_n + 3 (xyz PE + raw viewdirs); got %d", d.d_in);
     if (d.d_in > 16 * mlpk::NKB_IN) return fail(PNR_ERR_UNSUPPORTED, "d_in <= 64");
+    if (d.precision != PNR_PREC_F32 && d.precision != PNR_PREC_BF16X6 && d.precision != PNR_PREC_BF16X9)
+        return fail(PNR_ERR_UNSUPPORTED, "precision must be 0 (f32), 6 or 9 (split bf16); got %d", d.precision);
     return PNR_OK;
 }
 
@@ -458,12 +669,19 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
     const int64_t blocks = (L.total + 255) / 256;
     hipLaunchKernelGGL(mlpk::k_pack, dim3((unsigned)blocks), dim3(256), 0, st, s, L,
                        static_cast<float *>(packed));
-    return launch_ok("mlp_pack") ? PNR_OK : PNR_ERR_HIP;
+    if (!launch_ok("mlp_pack")) return PNR_ERR_HIP;
+    if (L.prec) {
+        const int64_t n = (int64_t)(mlpk::KS32_IN + L.n_l512 * mlpk::KS32) * mlpk::NRT * 64;
+        hipLaunchKernelGGL(mlpk::k_pack_split, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           s, L, static_cast<float *>(packed));
+        if (!launch_ok("mlp_pack_split")) return PNR_ERR_HIP;
+    }
+    return PNR_OK;
 }
 
 size_t mlp_xsum_bytes(int ns) {
-    if (ns <= 1) return 0;
-    return sizeof(float) * (size_t)device_cu_count() * mlpk::COLS * mlpk::H;
+    (void)ns;  // x park + multi-view sum, one pair of 128 KB regions per resident workgroup
+    return sizeof(float) * (size_t)device_cu_count() * 2 * mlpk::COLS * mlpk::H;
 }
 
 // Launch the fused model over n_points points (render mode if rays != nullptr).
@@ -488,7 +706,16 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
     const size_t lds = sizeof(float) * (size_t)mlpk::COLS * mlpk::LDS_LD;
-    hipLaunchKernelGGL(mlpk::k_point_mlp, dim3((unsigned)grid), dim3(256), lds, st, a);
+    switch (d.precision) {
+    case PNR_PREC_BF16X6:
+        hipLaunchKernelGGL(mlpk::k_point_mlp<6>, dim3((unsigned)grid), dim3(256), lds, st, a);
+        break;
+    case PNR_PREC_BF16X9:
+        hipLaunchKernelGGL(mlpk::k_point_mlp<9>, dim3((unsigned)grid), dim3(256), lds, st, a);
+        break;
+    default:
+        hipLaunchKernelGGL(mlpk::k_point_mlp<0>, dim3((unsigned)grid), dim3(256), lds, st, a);
+    }
     return launch_ok("point_mlp") ? PNR_OK : PNR_ERR_HIP;
 }
 

@@ -28,7 +28,8 @@ class Scene(ctypes.Structure):
 
 class MlpDesc(ctypes.Structure):
     _fields_ = [("d_in", c_i32), ("d_latent", c_i32), ("d_hidden", c_i32), ("d_out", c_i32),
-                ("n_blocks", c_i32), ("combine_layer", c_i32), ("pe_n", c_i32)]
+                ("n_blocks", c_i32), ("combine_layer", c_i32), ("pe_n", c_i32),
+                ("precision", c_i32)]
 
 
 class MlpWeights(ctypes.Structure):

@@ -21,7 +21,15 @@ from .conf import as_conf
 from .encoder import SpatialEncoder
 
 __all__ = ["PositionalEncoding", "ResnetBlockFC", "ResnetFC", "PixelNeRFNet", "make_model",
-           "make_mlp", "make_encoder"]
+           "make_mlp", "make_encoder", "PRECISIONS"]
+
+# Arithmetic of the 512-wide ResnetFC GEMMs (include/pnr_abi.h, PNR_PREC_*).  All modes
+# take fp32 in / fp32 out with fp32 accumulation:
+#   "fp32"   v_mfma_f32_16x16x4_f32
+#   "bf16x9" exact 3-way bf16 split of both operands, all 9 products (exact products,
+#            fp32 accumulation: numerically an fp32 GEMM)
+#   "bf16x6" the 6 largest products of that split (error at the fp32 unit roundoff)
+PRECISIONS = {"fp32": 0, "bf16x6": 6, "bf16x9": 9}
 
 
 class PositionalEncoding(nn.Module):
@@ -126,19 +134,19 @@ class ResnetFC(nn.Module):
             return "n_blocks > 8"
         return None
 
-    def desc(self, pe_n):
+    def desc(self, pe_n, precision="fp32"):
         return _lib.MlpDesc(self.d_in, self.d_latent, self.d_hidden, self.d_out, self.n_blocks,
-                            self.combine_layer, pe_n)
+                            self.combine_layer, pe_n, PRECISIONS[precision])
 
-    def packed(self, code):
+    def packed(self, code, precision="fp32"):
         """Packed fragment-order copy of the weights (re-packed when they change)."""
         params = [p for p in self.parameters()] + [code._freqs, code._phases]
-        key = tuple((p.data_ptr(), p._version) for p in params)
+        key = (precision,) + tuple((p.data_ptr(), p._version) for p in params)
         cache = self.__dict__.get("_pnr_pack")
         if cache is not None and cache[0] == key:
             return cache[1], cache[2]
         pe_n = int(code._freqs.numel())
-        desc = self.desc(pe_n)
+        desc = self.desc(pe_n, precision)
         lib = _lib.load()
         nbytes = lib.pnr_mlp_packed_bytes(desc)
         if nbytes == 0:
@@ -226,6 +234,9 @@ class PixelNeRFNet(nn.Module):
         self.register_buffer("cams", torch.empty(0, 16), persistent=False)
         self.num_objs = 0
         self.num_views_per_obj = 1
+        # GEMM arithmetic of the fused kernel (see PRECISIONS): the exact-split bf16x6 mode
+        # has fp32-level error at 1.7x the f32-MFMA throughput
+        self.mlp_precision = "bf16x6"
 
     # ---- encode ---------------------------------------------------------------------
     def encode(self, images, poses, focal, z_bounds=None, c=None):
@@ -340,7 +351,9 @@ class PixelNeRFNet(nn.Module):
 
     def hip_mlp(self, coarse):
         mlp = self.mlp_coarse if (coarse or self.mlp_fine is None) else self.mlp_fine
-        return mlp.packed(self.code)
+        if self.mlp_precision not in PRECISIONS:
+            raise ValueError("mlp_precision must be one of %s" % sorted(PRECISIONS))
+        return mlp.packed(self.code, self.mlp_precision)
 
     # ---- forward (point query) -----------------------------------------------------
     def forward(self, xyz, coarse=True, viewdirs=None, far=False):

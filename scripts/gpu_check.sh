@@ -15,4 +15,7 @@ ok $rc || exit $rc
 echo "== bench"; date
 timeout -k 10 600 python bench.py --steps ${BENCH_STEPS:-5} --warmup 1 > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
-exit $rc
+ok $rc || exit $rc
+echo "== precision study"; date
+timeout -k 10 300 python scripts/precision_study.py > gpurun_out/precision_study.json 2> gpurun_out/precision_study.err
+rc=$?; echo "prec rc=$rc"; exit $rc

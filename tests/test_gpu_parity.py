@@ -50,8 +50,12 @@ def model_conf(n_blocks=5, combine_layer=3):
                 mlp_fine=dict(mlp), encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
 
 
-def hip_net(cfg, arr):
+PRECS = ["fp32", "bf16x6", "bf16x9"]
+
+
+def hip_net(cfg, arr, precision="bf16x6"):
     net = PixelNeRFNet(model_conf(cfg.get("n_blocks", 5), cfg.get("combine_layer", 3)))
+    net.mlp_precision = precision
     if not cfg.get("with_fine", True):
         net.mlp_fine = None      # as eval_approx.py:62-63 does
     sd = fixtures.state_dict(cfg)
@@ -66,8 +70,8 @@ def hip_net(cfg, arr):
     return net
 
 
-def hip_render(cfg, arr, want_weights=True):
-    net = hip_net(cfg, arr)
+def hip_render(cfg, arr, want_weights=True, precision="bf16x6"):
+    net = hip_net(cfg, arr, precision)
     r = NeRFRenderer(n_coarse=cfg["n_coarse"], n_fine=cfg["n_fine"], n_fine_depth=cfg["n_fine_depth"],
                      depth_std=cfg["depth_std"], white_bkgd=cfg["white_bkgd"], lindisp=cfg["lindisp"])
     r.streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
@@ -156,10 +160,11 @@ def test_sample_fine_matches_oracle(kc, kf, kfd, lindisp):
 
 
 # ------------------------------------------------------------------- model --
-def test_point_query_matches_reference_fixture():
+@pytest.mark.parametrize("precision", PRECS)
+def test_point_query_matches_reference_fixture(precision):
     cfg, arr = fixtures.load("fw_pointquery")
     net = hip_net(dict(cfg, n_blocks=5, combine_layer=3, with_fine=True, d_latent=512,
-                       d_hidden=512), arr)
+                       d_hidden=512), arr, precision)
     with torch.no_grad():
         vd = torch.zeros_like(arr["xyz"]).to(DEV)
         oc = net(arr["xyz"].to(DEV), coarse=True, viewdirs=vd)
@@ -168,7 +173,8 @@ def test_point_query_matches_reference_fixture():
     assert_close(of, arr["out_fine"], "point query fine")
 
 
-def test_point_query_multiview_multiobject_vs_oracle():
+@pytest.mark.parametrize("precision", PRECS)
+def test_point_query_multiview_multiobject_vs_oracle(precision):
     """SB=2 objects x NS=3 views, per-object focal/c; checks the x_sum combine path."""
     torch.manual_seed(0)
     sb, ns, P = 2, 3, 200
@@ -183,6 +189,7 @@ def test_point_query_multiview_multiobject_vs_oracle():
     with torch.no_grad():
         ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, True, vd)
     net = PixelNeRFNet(model_conf())
+    net.mlp_precision = precision
     net.load_state_dict(sd, strict=False)
     net = net.to(DEV).eval()
     net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (64, 60), c=c.to(DEV), num_objs=sb)
@@ -219,12 +226,13 @@ def compare_render(name, out, cfg, arr):
     return frac
 
 
+@pytest.mark.parametrize("precision", PRECS)
 @pytest.mark.parametrize("name", ["fw_cfg2", "fw_shipped", "fw_cfg1", "fw_dtu_ns3"])
-def test_render_matches_reference_fixture(name):
+def test_render_matches_reference_fixture(name, precision):
     cfg, arr = fixtures.load(name)
-    out = hip_render(cfg, arr)
+    out = hip_render(cfg, arr, precision=precision)
     frac = compare_render(name, out, cfg, arr)
-    print("%s: fine-bin flip fraction %.4f" % (name, frac))
+    print("%s/%s: fine-bin flip fraction %.4f" % (name, precision, frac))
 
 
 def test_render_multiobject_vs_oracle():
