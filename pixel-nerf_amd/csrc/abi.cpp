@@ -67,6 +67,8 @@ static int check_scene(const pnr_scene *sc) {
     if (!(sc->image_w > 0.f) || !(sc->image_h > 0.f)) return fail(PNR_ERR_INVALID, "image size <= 0");
     if ((reinterpret_cast<uintptr_t>(sc->latent) & 15) != 0)
         return fail(PNR_ERR_INVALID, "latent must be 16-byte aligned");
+    if ((int64_t)sc->n_obj * sc->n_views * sc->latent_h * sc->latent_w * sc->latent_c >= (1ll << 32))
+        return fail(PNR_ERR_UNSUPPORTED, "latent larger than 2^32 floats (32-bit gather offsets)");
     return PNR_OK;
 }
 

@@ -251,6 +251,15 @@ __device__ __forceinline__ unsigned cvt_pk(float a, float b) {
 }
 __device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 &x1, bf8 &x2) {
     const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+#ifdef PNR_ABLATE_SPLIT
+    {   // diagnostic: hi part only (wrong numerics), no split VALU
+        u4 p;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = cvt_pk(x[2 * q], x[2 * q + 1]);
+        x0 = x1 = x2 = __builtin_bit_cast(bf8, p);
+        return;
+    }
+#endif
     u4 p0, p1, p2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -268,49 +277,70 @@ __device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 
     x2 = __builtin_bit_cast(bf8, p2);
 }
 
+// workgroup barrier that waits only for LDS traffic: a __syncthreads() would also
+// emit s_waitcnt vmcnt(0) and drain the weight prefetch that spans k-steps
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+constexpr int STG_FLOATS = CT * 3 * 256;   // one staging buffer: [ct][part][lane][8 bf16]
+
 // Split-bf16 GEMM: acc[r][c] += sum over the NTERM largest products of the exact
 // 3-way splits of W and IN (6 terms: error ~ fp32 unit roundoff; 9 terms: every
 // product exact, only fp32 accumulation rounds) on v_mfma_f32_16x16x32_bf16.
-//   wp  : packed layer + this wave's first row tile + lane*4 (floats)
-//   inb : LDS buffer at (column cl, k 8g) of this lane
-// Software pipeline: A fragments stream from L2 three row tiles ahead into a
-// 4-deep register ring; the B fragments of k-step ks+1 are read from LDS at the
-// top of ks and split halfway through ks, so the split VALU overlaps the MFMAs.
+//   wp   : packed layer + this wave's first row tile + lane*4 (floats)
+//   inbw : LDS activations at (column 16*wave + cl, k 8g): the tile this wave splits
+//   stg  : LDS staging ring, 2 x [ct][part][lane][8 bf16] (24 KB)
+// Each wave splits ONE column tile of the next k-step into the staging ring (a
+// quarter of the split VALU) and all waves read every tile's parts from it; A
+// fragments stream from L2 three row tiles ahead into a 4-deep register ring.
 template <int NKS, int NTERM>
-__device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ wp, const float *inb) {
+__device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ wp, const float *inbw,
+                                           float *stg, int wave, int lane) {
     bf8 ra[4][3];
     auto loadA = [&](bf8 (&dst)[3], int ks, int r) {
+#ifdef PNR_ABLATE_WSTREAM
+        ks = 0;  // diagnostic: every k-step re-reads k-step 0 (L1/L2-hot), no weight stream
+#endif
         const float *src = wp + (int64_t)ks * SKS_FLOATS + r * SRT_FLOATS;
 #pragma unroll
         for (int q = 0; q < 3; ++q) dst[q] = *reinterpret_cast<const bf8 *>(src + q * 256);
     };
-    auto loadB = [&](f4 (&dst)[CT][2], int ks) {
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const float *bp = inb + c * 16 * LDS_LD + 32 * ks;
-            dst[c][0] = *reinterpret_cast<const f4 *>(bp);
-            dst[c][1] = *reinterpret_cast<const f4 *>(bp + 4);
-        }
+    auto split_own = [&](int ks, int buf) {
+        const float *bp = inbw + 32 * ks;
+        const f4 lo = *reinterpret_cast<const f4 *>(bp);
+        const f4 hi = *reinterpret_cast<const f4 *>(bp + 4);
+        bf8 p0, p1, p2;
+        split3(lo, hi, p0, p1, p2);
+        float *d = stg + buf * STG_FLOATS + wave * 768 + lane * 4;
+        *reinterpret_cast<bf8 *>(d) = p0;
+        *reinterpret_cast<bf8 *>(d + 256) = p1;
+        *reinterpret_cast<bf8 *>(d + 512) = p2;
     };
-    bf8 b0[CT], b1[CT], b2[CT];
-    {
-        f4 braw[CT][2];
-        loadB(braw, 0);
-#pragma unroll
-        for (int c = 0; c < CT; ++c) split3(braw[c][0], braw[c][1], b0[c], b1[c], b2[c]);
-    }
+    split_own(0, 0);
     loadA(ra[0], 0, 0);
     loadA(ra[1], 0, 1);
     loadA(ra[2], 0, 2);
+    lds_barrier();
 #pragma unroll 1
     for (int ks = 0; ks < NKS; ++ks) {
-        // branch-free: the last k-step re-reads its own fragments instead of testing
-        const int kn = ks + 1 < NKS ? ks + 1 : ks;
-        f4 braw[CT][2];
-        loadB(braw, kn);
-        bf8 n0[CT], n1[CT], n2[CT];
+        const int kn = ks + 1 < NKS ? ks + 1 : ks;   // branch-free tail: redundant re-split
+        bf8 b0[CT], b1[CT], b2[CT];
+        const float *sp = stg + (ks & 1) * STG_FLOATS + lane * 4;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+#ifdef PNR_ABLATE_STGREAD
+            b0[c] = ra[0][c % 3]; b1[c] = ra[1][c % 3]; b2[c] = ra[2][c % 3];  // diagnostic
+#else
+            b0[c] = *reinterpret_cast<const bf8 *>(sp + c * 768);
+            b1[c] = *reinterpret_cast<const bf8 *>(sp + c * 768 + 256);
+            b2[c] = *reinterpret_cast<const bf8 *>(sp + c * 768 + 512);
+#endif
+        }
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
+            // split after the first row tile so its LDS reads don't gate the k-step start
+            if (r == 1) split_own(kn, (ks + 1) & 1);
             const int rn = r + 3;
             if (rn < RTW) loadA(ra[rn & 3], ks, rn);
             else loadA(ra[rn & 3], kn, rn - RTW);
@@ -334,17 +364,10 @@ __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ w
                 v = mfma_bf(a[0], b0[c], v);
                 acc[r][c] = v;
             }
-            if (r == 2) {
-#pragma unroll
-                for (int c = 0; c < CT; ++c) split3(braw[c][0], braw[c][1], n0[c], n1[c], n2[c]);
-            }
         }
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            b0[c] = n0[c];
-            b1[c] = n1[c];
-            b2[c] = n2[c];
-        }
+#ifndef PNR_ABLATE_KBARRIER
+        lds_barrier();
+#endif
     }
 }
 
@@ -359,6 +382,10 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
     }
 }
 
+#ifndef PNR_PARK_X
+#define PNR_PARK_X 0
+#endif
+constexpr bool kParkX = PNR_PARK_X;
 // x parks in scratch while h occupies the accumulator registers (frees 128 regs
 // for the operand pipelines); each (r, c) is one coalesced 1 KB wave store / load
 __device__ __forceinline__ void park(const Acc &acc, float *xp) {
@@ -387,11 +414,18 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
         }
 }
 
+struct GemmCtx {
+    int64_t wl_off, ws_off;   // f32 / split fragment offsets of this wave + lane
+    const float *inb4;        // f32 B: column 16c + cl, k 16kb + 4g
+    const float *inbw;        // split: own column tile 16*wave + cl, k 8g
+    float *stg;               // split staging ring
+    int wave, lane;
+};
+
 template <int PREC, int NK>
-__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, int64_t wl_off,
-                                           int64_t ws_off, const float *inb4, const float *inb8) {
-    if constexpr (PREC == 0) gemm<NK>(acc, layer_base + wl_off, inb4);
-    else gemm_split<NK / 2, PREC>(acc, layer_base + ws_off, inb8);
+__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, const GemmCtx &g) {
+    if constexpr (PREC == 0) gemm<NK>(acc, layer_base + g.wl_off, g.inb4);
+    else gemm_split<NK / 2, PREC>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane);
 }
 
 template <int PREC>
@@ -412,7 +446,15 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
     const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;         // f32 fragments
     const int64_t ws_off = (int64_t)(RTW * wave) * SRT_FLOATS + lane * 4;  // split fragments
     const float *inb = inbuf + cl * LDS_LD + 4 * g;     // B (f32): column 16c + cl, k 16kb + 4g
-    const float *inb8 = inbuf + cl * LDS_LD + 8 * g;    // B (split): k 32ks + 8g
+    GemmCtx gc;
+    gc.wl_off = wl_off;
+    gc.ws_off = ws_off;
+    gc.inb4 = inb;
+    gc.inbw = inbuf + (16 * wave + cl) * LDS_LD + 8 * g;
+    gc.stg = inbuf + COLS * LDS_LD;
+    float *gtab = gc.stg + 2 * STG_FLOATS;   // per-column gather records (64 x 8 floats)
+    gc.wave = wave;
+    gc.lane = lane;
     // feature / gather role: thread -> (column col, quarter qt)
     const int col = tid >> 2, qt = tid & 3;
 
@@ -501,46 +543,66 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             const int x1 = x0 + 1 < a.wl ? x0 + 1 : x0, y1 = y0 + 1 < a.hl ? y0 + 1 : y0;
             if (x0 + 1 >= a.wl) { wne = 0.f; wse = 0.f; }
             if (y0 + 1 >= a.hl) { wsw = 0.f; wse = 0.f; }
-            const float *lat = a.latent + (obj * a.ns + v) * (int64_t)a.hl * a.wl * H + 128 * qt;
-            const f4 *cnw = reinterpret_cast<const f4 *>(lat + ((int64_t)y0 * a.wl + x0) * H);
-            const f4 *cne = reinterpret_cast<const f4 *>(lat + ((int64_t)y0 * a.wl + x1) * H);
-            const f4 *csw = reinterpret_cast<const f4 *>(lat + ((int64_t)y1 * a.wl + x0) * H);
-            const f4 *cse = reinterpret_cast<const f4 *>(lat + ((int64_t)y1 * a.wl + x1) * H);
+            if (qt == 0) {
+                // per-column gather record: 4 corner offsets (floats from a.latent) + weights
+                const uint32_t base = (uint32_t)((obj * a.ns + v) * (int64_t)a.hl * a.wl * H);
+                const uint32_t o00 = base + (uint32_t)(y0 * a.wl + x0) * H, o01 = base + (uint32_t)(y0 * a.wl + x1) * H;
+                const uint32_t o10 = base + (uint32_t)(y1 * a.wl + x0) * H, o11 = base + (uint32_t)(y1 * a.wl + x1) * H;
+                float *t = gtab + col * 8;
+                *reinterpret_cast<f4 *>(t) = f4{__uint_as_float(o00), __uint_as_float(o01),
+                                                __uint_as_float(o10), __uint_as_float(o11)};
+                *reinterpret_cast<f4 *>(t + 4) = f4{wnw, wne, wsw, wse};
+            }
             __syncthreads();   // features visible
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, g, false);
-            layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, wl_off, ws_off, inb, inb8);
+            layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, gc);
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
                 __syncthreads();
-                // z = bilinear latent gather (torch's nw, ne, sw, se summation order),
-                // channels [128 qt, 128 qt + 128) of this thread's column
+                // z = bilinear latent gather (torch's nw, ne, sw, se summation order).
+                // Wave w walks its 16 columns; each load instruction reads one contiguous
+                // 1 KB half of a corner's 2 KB channel row (lane = 4 channels).
 #pragma unroll 4
-                for (int m = 0; m < 32; ++m) {
-                    const f4 c0 = cnw[m], c1 = cne[m], c2 = csw[m], c3 = cse[m];
-                    f4 zz;
+                for (int j = 0; j < 16; ++j) {
+                    const int cj = 16 * wave + j;
+                    const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
+                    const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        zz[j] = add_rn(add_rn(add_rn(mul_rn(c0[j], wnw), mul_rn(c1[j], wne)),
-                                              mul_rn(c2[j], wsw)), mul_rn(c3[j], wse));
-                    *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + 128 * qt + 4 * m) = zz;
+                    for (int half = 0; half < 2; ++half) {
+                        const uint32_t ch = half * 256 + lane * 4;
+#ifdef PNR_ABLATE_GATHER
+                        const f4 c0 = tw, c1 = to, c2 = tw, c3 = to;  // diagnostic
+#else
+                        const f4 c0 = *reinterpret_cast<const f4 *>(a.latent + __float_as_uint(to.x) + ch);
+                        const f4 c1 = *reinterpret_cast<const f4 *>(a.latent + __float_as_uint(to.y) + ch);
+                        const f4 c2 = *reinterpret_cast<const f4 *>(a.latent + __float_as_uint(to.z) + ch);
+                        const f4 c3 = *reinterpret_cast<const f4 *>(a.latent + __float_as_uint(to.w) + ch);
+#endif
+                        f4 zz;
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            zz[q] = add_rn(add_rn(add_rn(mul_rn(c0[q], tw.x), mul_rn(c1[q], tw.y)),
+                                                  mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
+                        *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
+                    }
                 }
                 __syncthreads();
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
-                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, wl_off, ws_off, inb, inb8);
+                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc);
                 __syncthreads();
                 store_relu(x, inbuf, wave, lane);
-                if constexpr (PREC != 0) park(x, xp);
+                if constexpr (PREC != 0 && kParkX) park(x, xp);
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, g, false);
-                layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, wl_off, ws_off, inb, inb8);
+                layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc);
                 __syncthreads();
                 store_relu(h, inbuf, wave, lane);
                 __syncthreads();
-                if constexpr (PREC != 0) unpark(x, xp);
+                if constexpr (PREC != 0 && kParkX) unpark(x, xp);
                 add_bias(x, bias + (3 + lz) * H, wave, g, true);
-                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, wl_off, ws_off, inb, inb8);
+                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -575,16 +637,16 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             __syncthreads();
             store_relu(x, inbuf, wave, lane);
-            if constexpr (PREC != 0) park(x, xp);
+            if constexpr (PREC != 0 && kParkX) park(x, xp);
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, g, false);
-            layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, wl_off, ws_off, inb, inb8);
+            layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc);
             __syncthreads();
             store_relu(h, inbuf, wave, lane);
             __syncthreads();
-            if constexpr (PREC != 0) unpark(x, xp);
+            if constexpr (PREC != 0 && kParkX) unpark(x, xp);
             add_bias(x, bias + (2 + l0) * H, wave, g, true);
-            layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, wl_off, ws_off, inb, inb8);
+            layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w -> columns 16w..
         __syncthreads();
@@ -705,7 +767,8 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
-    const size_t lds = sizeof(float) * (size_t)mlpk::COLS * mlpk::LDS_LD;
+    const size_t lds = sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS +
+                                        mlpk::COLS * 8);
     switch (d.precision) {
     case PNR_PREC_BF16X6:
         hipLaunchKernelGGL(mlpk::k_point_mlp<6>, dim3((unsigned)grid), dim3(256), lds, st, a);

@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (load torch's HIP runtime before libpnr.so)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpnr.so")
+# PNR_LIB_PATH: alternate build (diagnostic ablation builds only)
+LIB_PATH = os.environ.get("PNR_LIB_PATH") or os.path.join(_HERE, "libpnr.so")
 
 c_f = ctypes.c_float
 c_i32 = ctypes.c_int32
