@@ -284,6 +284,11 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 constexpr int STG_FLOATS = CT * 3 * 256;   // one staging buffer: [ct][part][lane][8 bf16]
+#ifndef PNR_A_DIST
+#define PNR_A_DIST 3
+#endif
+constexpr int A_DIST = PNR_A_DIST;                 // weight prefetch distance (row tiles)
+constexpr int A_RING = A_DIST < 4 ? 4 : 8;         // register ring (divides RTW = 8)
 
 // Split-bf16 GEMM: acc[r][c] += sum over the NTERM largest products of the exact
 // 3-way splits of W and IN (6 terms: error ~ fp32 unit roundoff; 9 terms: every
@@ -297,7 +302,7 @@ constexpr int STG_FLOATS = CT * 3 * 256;   // one staging buffer: [ct][part][lan
 template <int NKS, int NTERM>
 __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ wp, const float *inbw,
                                            float *stg, int wave, int lane) {
-    bf8 ra[4][3];
+    bf8 ra[A_RING][3];
     auto loadA = [&](bf8 (&dst)[3], int ks, int r) {
 #ifdef PNR_ABLATE_WSTREAM
         ks = 0;  // diagnostic: every k-step re-reads k-step 0 (L1/L2-hot), no weight stream
@@ -318,9 +323,8 @@ __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ w
         *reinterpret_cast<bf8 *>(d + 512) = p2;
     };
     split_own(0, 0);
-    loadA(ra[0], 0, 0);
-    loadA(ra[1], 0, 1);
-    loadA(ra[2], 0, 2);
+#pragma unroll
+    for (int r = 0; r < A_DIST; ++r) loadA(ra[r], 0, r);
     lds_barrier();
 #pragma unroll 1
     for (int ks = 0; ks < NKS; ++ks) {
@@ -341,13 +345,13 @@ __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ w
         for (int r = 0; r < RTW; ++r) {
             // split after the first row tile so its LDS reads don't gate the k-step start
             if (r == 1) split_own(kn, (ks + 1) & 1);
-            const int rn = r + 3;
-            if (rn < RTW) loadA(ra[rn & 3], ks, rn);
-            else loadA(ra[rn & 3], kn, rn - RTW);
+            const int rn = r + A_DIST;
+            if (rn < RTW) loadA(ra[rn % A_RING], ks, rn);
+            else loadA(ra[rn % A_RING], kn, rn - RTW);
             // keep the prefetch where it is: without the barrier the scheduler sinks
             // the loads next to their use to save registers and serializes the ring
             __builtin_amdgcn_sched_barrier(0);
-            const bf8 *a = ra[r & 3];
+            const bf8 *a = ra[r % A_RING];
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
                 f4 v = acc[r][c];
