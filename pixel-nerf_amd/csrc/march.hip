@@ -122,6 +122,9 @@ __global__ __launch_bounds__(64) void k_sample_fine(
 // One wave per ray, 4 rays per 256-thread block; the cumprod is a double-precision
 // wave scan (torch's CPU cumprod accumulates in double and rounds each prefix).
 // ---------------------------------------------------------------------------
+// NCH > 0: K <= 64 NCH, every chunk's loads are issued before the first scan (more
+// bytes in flight per wave: the kernel is HBM-bound); NCH == 0: any K, chunk loop.
+template <int NCH>
 __global__ __launch_bounds__(256) void k_composite(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
     int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
@@ -132,20 +135,32 @@ __global__ __launch_bounds__(256) void k_composite(
     const float far = rays[b * 8 + 7];
     const float *zr = z + b * K;
     const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
+    constexpr int NR = NCH > 0 ? NCH : 1;
+    float zk[NR], zn[NR];
+    f4 v[NR];
+    auto load = [&](int i, int k) {
+        zk[i] = 0.f;
+        zn[i] = 0.f;
+        v[i] = f4{0.f, 0.f, 0.f, 0.f};
+        if (k < K) {
+            zk[i] = __builtin_nontemporal_load(zr + k);
+            zn[i] = (k + 1 < K) ? zr[k + 1] : far;
+            const float *rp = reinterpret_cast<const float *>(rr + k);
+            v[i] = f4{__builtin_nontemporal_load(rp), __builtin_nontemporal_load(rp + 1),
+                      __builtin_nontemporal_load(rp + 2), __builtin_nontemporal_load(rp + 3)};
+        }
+    };
+    if constexpr (NCH > 0) {
+#pragma unroll
+        for (int i = 0; i < NCH; ++i) load(i, 64 * i + lane);
+    }
     double carry = 1.0;
     float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
-    for (int c0 = 0; c0 < K; c0 += 64) {
-        const int k = c0 + lane;
+    auto step = [&](int c, int i) {
+        const int k = 64 * c + lane;
         const bool valid = k < K;
-        float zk = 0.f, zn = 0.f;
-        f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (valid) {
-            zk = zr[k];
-            zn = (k + 1 < K) ? zr[k + 1] : far;
-            v = rr[k];
-        }
-        const float delta = sub_rn(zn, zk);
-        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v.w, 0.0f)))) : 0.0f;
+        const float delta = sub_rn(zn[i], zk[i]);
+        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v[i].w, 0.0f)))) : 0.0f;
         const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
         double p = shifted;  // inclusive product scan
 #pragma unroll
@@ -159,12 +174,21 @@ __global__ __launch_bounds__(256) void k_composite(
         const float wk = mul_rn(alpha, T);
         carry *= __shfl(p, 63, 64);
         if (valid) {
-            if (weights) weights[b * K + k] = wk;
-            sr += mul_rn(wk, v.x);
-            sg += mul_rn(wk, v.y);
-            sb += mul_rn(wk, v.z);
-            sd += mul_rn(wk, zk);
+            if (weights) __builtin_nontemporal_store(wk, weights + b * K + k);
+            sr += mul_rn(wk, v[i].x);
+            sg += mul_rn(wk, v[i].y);
+            sb += mul_rn(wk, v[i].z);
+            sd += mul_rn(wk, zk[i]);
             sw += wk;
+        }
+    };
+    if constexpr (NCH > 0) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) step(c, c);
+    } else {
+        for (int c = 0; c < (K + 63) / 64; ++c) {
+            load(0, 64 * c + lane);
+            step(c, 0);
         }
     }
     sr = wave_sum(sr);
@@ -221,7 +245,10 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
                      int white_bkgd, float *weights, float *rgb, float *depth, hipStream_t st) {
     if (n_rays == 0) return PNR_OK;
     const int64_t blocks = (n_rays + 3) / 4;
-    hipLaunchKernelGGL(k_composite, dim3((unsigned)blocks), dim3(256), 0, st, z, raw, rays,
+    const int nch = (K + 63) / 64;
+    auto kern = nch == 1 ? k_composite<1> : nch == 2 ? k_composite<2> : nch == 3 ? k_composite<3>
+              : nch == 4 ? k_composite<4> : k_composite<0>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, z, raw, rays,
                        n_rays, K, white_bkgd, weights, rgb, depth);
     return launch_ok("composite") ? PNR_OK : PNR_ERR_HIP;
 }

@@ -418,18 +418,41 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
         }
 }
 
+// Diagnostic build only (-DPNR_PHASE_TIMING, scripts/build_variant.sh): wave-0 shader
+// cycles per phase, summed over workgroups: 0 features/projection, 1 latent gather,
+// 2 GEMMs, 3 glue (bias, relu stores, barriers), 4 lin_out head, 5 GEMM calls, 6 tiles.
+#ifdef PNR_PHASE_TIMING
+__device__ unsigned long long g_phase[8];
+#define PT(gc, i)                                                     \
+    do {                                                              \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
+        (gc).pt[i] += t_ - (gc).pt_last;                              \
+        (gc).pt_last = t_;                                            \
+    } while (0)
+#define PT_COUNT(gc, i) ((gc).pt[i] += 1)
+#else
+#define PT(gc, i) ((void)0)
+#define PT_COUNT(gc, i) ((void)0)
+#endif
+
 struct GemmCtx {
     int64_t wl_off, ws_off;   // f32 / split fragment offsets of this wave + lane
     const float *inb4;        // f32 B: column 16c + cl, k 16kb + 4g
     const float *inbw;        // split: own column tile 16*wave + cl, k 8g
     float *stg;               // split staging ring
     int wave, lane;
+#ifdef PNR_PHASE_TIMING
+    uint64_t pt[8], pt_last;
+#endif
 };
 
 template <int PREC, int NK>
-__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, const GemmCtx &g) {
+__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g) {
+    PT(g, 3);
+    PT_COUNT(g, 5);
     if constexpr (PREC == 0) gemm<NK>(acc, layer_base + g.wl_off, g.inb4);
     else gemm_split<NK / 2, PREC>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane);
+    PT(g, 2);
 }
 
 template <int PREC>
@@ -459,6 +482,10 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
     float *gtab = gc.stg + 2 * STG_FLOATS;   // per-column gather records (64 x 8 floats)
     gc.wave = wave;
     gc.lane = lane;
+#ifdef PNR_PHASE_TIMING
+    for (int i = 0; i < 8; ++i) gc.pt[i] = 0;
+    gc.pt_last = __builtin_amdgcn_s_memtime();
+#endif
     // feature / gather role: thread -> (column col, quarter qt)
     const int col = tid >> 2, qt = tid & 3;
 
@@ -558,6 +585,7 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                 *reinterpret_cast<f4 *>(t + 4) = f4{wnw, wne, wsw, wse};
             }
             __syncthreads();   // features visible
+            PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, g, false);
             layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, gc);
@@ -565,6 +593,7 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
                 __syncthreads();
+                PT(gc, 3);
                 // z = bilinear latent gather (torch's nw, ne, sw, se summation order).
                 // Wave w walks its 16 columns; each load instruction reads one contiguous
                 // 1 KB half of a corner's 2 KB channel row (lane = 4 channels).
@@ -593,6 +622,7 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                     }
                 }
                 __syncthreads();
+                PT(gc, 1);
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc);
                 __syncthreads();
@@ -656,6 +686,7 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
         __syncthreads();
         store_relu(x, inbuf, wave, lane);
         __syncthreads();
+        PT(gc, 3);
         {
             const float *wo = a.packed + L.off_lin_out + lane * 4;
             const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
@@ -681,7 +712,13 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                 *reinterpret_cast<f4 *>(a.out + po * 4) = r;
             }
         }
+        PT(gc, 4);
+        PT_COUNT(gc, 6);
     }
+#ifdef PNR_PHASE_TIMING
+    if (threadIdx.x == 0)
+        for (int i = 0; i < 8; ++i) atomicAdd(&g_phase[i], (unsigned long long)gc.pt[i]);
+#endif
 }
 
 }  // namespace mlpk
@@ -689,6 +726,18 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
 // ------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------
+#ifdef PNR_PHASE_TIMING
+// diagnostic: copy (and optionally clear) the phase counters; not part of the ABI
+extern "C" int pnr_debug_phase(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mlpk::g_phase), sizeof(unsigned long long) * 8) != hipSuccess)
+        return -1;
+    if (reset) {
+        static const unsigned long long zero[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mlpk::g_phase), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 size_t mlp_packed_bytes(const pnr_mlp_desc &d) {
     return sizeof(float) * (size_t)mlpk::make_layout(d).total;
 }

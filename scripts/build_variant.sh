@@ -1,0 +1,29 @@
+#!/bin/bash
+# Build an A/B variant of libpnr.so into pixel-nerf_amd/build/<tag>/libpnr.so.
+#   scripts/build_variant.sh <tag> <git-rev|WORKTREE> [extra hipcc flags...]
+# The csrc/ sources come from <rev> (or the working tree); select the variant at run
+# time with PNR_LIB_PATH=pixel-nerf_amd/build/<tag>/libpnr.so (diagnostic only).
+set -euo pipefail
+tag=$1; rev=$2; shift 2
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/pixel-nerf_amd/build/$tag
+src=$out/src
+rm -rf "$out"; mkdir -p "$src/csrc" "$src/include"
+for f in march.hip mlp.hip abi.cpp pnr_common.h; do
+  if [ "$rev" = WORKTREE ]; then cp "$root/pixel-nerf_amd/csrc/$f" "$src/csrc/$f"
+  else git -C "$root" show "$rev:pixel-nerf_amd/csrc/$f" > "$src/csrc/$f"; fi
+done
+if [ "$rev" = WORKTREE ]; then cp "$root/include/pnr_abi.h" "$src/include/"
+else git -C "$root" show "$rev:include/pnr_abi.h" > "$src/include/pnr_abi.h"; fi
+# sources include "../../include/pnr_abi.h" relative to csrc/
+mkdir -p "$out/include"; cp "$src/include/pnr_abi.h" "$out/include/"
+objs=()
+for f in march.hip mlp.hip abi.cpp; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w "$@" -I"$src/csrc" \
+    -x hip -c "$src/csrc/$f" -o "$out/$f.o" &
+  objs+=("$out/$f.o")
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libpnr.so" "${objs[@]}" \
+  -Wl,-rpath,/opt/rocm/lib
+echo "built $out/libpnr.so"

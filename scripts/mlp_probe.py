@@ -17,12 +17,32 @@ net.mlp_precision = prec
 r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True)
 import time  # noqa: E402
 
+import ctypes  # noqa: E402
+from pnr import _lib  # noqa: E402
+
+dbg = getattr(_lib.load(), "pnr_debug_phase", None)   # PNR_PHASE_TIMING variant only
+ph = (ctypes.c_ulonglong * 8)()
 with torch.no_grad():
     r(net, rays[:4096][None])
     torch.cuda.synchronize()
+    if dbg is not None:
+        dbg(ph, 1)
     t0 = time.perf_counter()
     for i in range(n):
         r(net, rays[:4096][None])
     torch.cuda.synchronize()
 print("done", prec, n, "chunk_ms %.3f" % ((time.perf_counter() - t0) / n * 1e3),
       os.environ.get("PNR_LIB_PATH", "default"))
+if dbg is not None:
+    dbg(ph, 0)
+    v = list(ph)
+    names = ["features", "gather", "gemm", "glue", "head"]
+    tot = sum(v[:5])
+    print("phase cycles/tile (wave 0):", {nm: round(v[i] / v[6]) for i, nm in enumerate(names)},
+          "share:", {nm: round(v[i] / tot, 4) for i, nm in enumerate(names)},
+          "gemm cycles/call: %.0f" % (v[2] / v[5]), "calls", v[5], "tiles", v[6])
+
+if os.environ.get("COMPOSITE"):
+    with torch.no_grad():
+        c = bench.composite_roofline(dev, bench.HipEvents())
+    print("composite", {k: (v["ms"], v["frac"]) for k, v in c.items()})
