@@ -28,8 +28,13 @@ constexpr int H = 512;             // d_hidden == d_latent (only width implement
 constexpr int NRT = H / 16;        // 32 row tiles per layer
 constexpr int NKB = H / 16;        // 32 k-blocks (16 k each) for K = 512
 constexpr int NKB_IN = 4;          // lin_in k-blocks (d_in <= 64, zero padded)
-constexpr int WAVES = 4;
-constexpr int RTW = NRT / WAVES;   // 8 row tiles per wave
+#ifndef PNR_WAVES
+#define PNR_WAVES 8
+#endif
+constexpr int WAVES = PNR_WAVES;   // 8: two waves per SIMD (4: one)
+constexpr int NTHR = 64 * WAVES;
+constexpr int RTW = NRT / WAVES;   // row tiles per wave (4 at 8 waves)
+static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves per workgroup");
 constexpr int CT = 4;              // column tiles (16 columns each)
 constexpr int COLS = 16 * CT;      // 64 points per tile
 constexpr int LDS_LD = H + 4;      // floats per column in the LDS activation buffer
@@ -249,6 +254,16 @@ __device__ __forceinline__ unsigned cvt_pk(float a, float b) {
     bf2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, bf2);
     return __builtin_bit_cast(unsigned, v);
 }
+// one pair (a, b) -> the packed bf16 pairs of its three parts
+__device__ __forceinline__ void split_pair(float a, float b, unsigned &p0, unsigned &p1, unsigned &p2) {
+    const unsigned h = cvt_pk(a, b);
+    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+    const unsigned m = cvt_pk(ra, rb);
+    const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
+    p0 = h;
+    p1 = m;
+    p2 = cvt_pk(sa, sb);
+}
 __device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 &x1, bf8 &x2) {
     const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #ifdef PNR_ABLATE_SPLIT
@@ -263,14 +278,11 @@ __device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 
     u4 p0, p1, p2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const float a = x[2 * q], b = x[2 * q + 1];
-        const unsigned h = cvt_pk(a, b);
-        const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
-        const unsigned m = cvt_pk(ra, rb);
-        const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
-        p0[q] = h;
-        p1[q] = m;
-        p2[q] = cvt_pk(sa, sb);
+        unsigned a, b, c;
+        split_pair(x[2 * q], x[2 * q + 1], a, b, c);
+        p0[q] = a;
+        p1[q] = b;
+        p2[q] = c;
     }
     x0 = __builtin_bit_cast(bf8, p0);
     x1 = __builtin_bit_cast(bf8, p1);
@@ -311,16 +323,30 @@ __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ w
 #pragma unroll
         for (int q = 0; q < 3; ++q) dst[q] = *reinterpret_cast<const bf8 *>(src + q * 256);
     };
+    // 4 waves: wave w splits all 8 k of column tile w; 8 waves: wave w splits the
+    // k-half w / 4 (4 values per lane) of column tile w % 4
     auto split_own = [&](int ks, int buf) {
         const float *bp = inbw + 32 * ks;
-        const f4 lo = *reinterpret_cast<const f4 *>(bp);
-        const f4 hi = *reinterpret_cast<const f4 *>(bp + 4);
-        bf8 p0, p1, p2;
-        split3(lo, hi, p0, p1, p2);
-        float *d = stg + buf * STG_FLOATS + wave * 768 + lane * 4;
-        *reinterpret_cast<bf8 *>(d) = p0;
-        *reinterpret_cast<bf8 *>(d + 256) = p1;
-        *reinterpret_cast<bf8 *>(d + 512) = p2;
+        if constexpr (WAVES == 4) {
+            const f4 lo = *reinterpret_cast<const f4 *>(bp);
+            const f4 hi = *reinterpret_cast<const f4 *>(bp + 4);
+            bf8 p0, p1, p2;
+            split3(lo, hi, p0, p1, p2);
+            float *d = stg + buf * STG_FLOATS + wave * 768 + lane * 4;
+            *reinterpret_cast<bf8 *>(d) = p0;
+            *reinterpret_cast<bf8 *>(d + 256) = p1;
+            *reinterpret_cast<bf8 *>(d + 512) = p2;
+        } else {
+            const f4 v = *reinterpret_cast<const f4 *>(bp);
+            unsigned a0, a1, a2, b0, b1, b2;
+            split_pair(v.x, v.y, a0, a1, a2);
+            split_pair(v.z, v.w, b0, b1, b2);
+            typedef unsigned u2 __attribute__((ext_vector_type(2)));
+            float *d = stg + buf * STG_FLOATS + (wave % CT) * 768 + lane * 4 + 2 * (wave / CT);
+            *reinterpret_cast<u2 *>(d) = u2{a0, b0};
+            *reinterpret_cast<u2 *>(d + 256) = u2{a1, b1};
+            *reinterpret_cast<u2 *>(d + 512) = u2{a2, b2};
+        }
     };
     split_own(0, 0);
 #pragma unroll
@@ -456,7 +482,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
 }
 
 template <int PREC>
-__global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
+__global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
     const int tid = threadIdx.x;
@@ -477,7 +503,7 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
     gc.wl_off = wl_off;
     gc.ws_off = ws_off;
     gc.inb4 = inb;
-    gc.inbw = inbuf + (16 * wave + cl) * LDS_LD + 8 * g;
+    gc.inbw = inbuf + (16 * (wave % CT) + cl) * LDS_LD + 8 * g + 4 * (wave / CT);
     gc.stg = inbuf + COLS * LDS_LD;
     float *gtab = gc.stg + 2 * STG_FLOATS;   // per-column gather records (64 x 8 floats)
     gc.wave = wave;
@@ -486,8 +512,9 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
     for (int i = 0; i < 8; ++i) gc.pt[i] = 0;
     gc.pt_last = __builtin_amdgcn_s_memtime();
 #endif
-    // feature / gather role: thread -> (column col, quarter qt)
-    const int col = tid >> 2, qt = tid & 3;
+    // feature role: thread -> (column col, part qt of WAVES); FPT features each
+    constexpr int FPT = 64 / WAVES;
+    const int col = tid / WAVES, qt = tid % WAVES;
 
     Acc x, h;
     for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
@@ -527,14 +554,14 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                 xc[i] = add_rn(xr[i], cam[9 + i]);
             }
             const float fx = cam[12], fy = cam[13], cx = cam[14], cy = cam[15];
-            // features f = 16 qt .. 16 qt + 15 of [xyz_rot | PE | viewdir_cam | 0]
+            // features f = FPT qt .. FPT qt + FPT - 1 of [xyz_rot | PE | viewdir_cam | 0]
             __syncthreads();   // previous users of inbuf are done
             {
                 const int npe = 3 * L.pe_n;
-                float fv[16];
+                float fv[FPT];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int f = 16 * qt + i;
+                for (int i = 0; i < FPT; ++i) {
+                    const int f = FPT * qt + i;
                     float val = 0.f;
                     if (f < 3) val = xr[f];
                     else if (f < 3 + npe) {
@@ -548,8 +575,8 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                     fv[i] = val;
                 }
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + 16 * qt + 4 * i) =
+                for (int i = 0; i < FPT / 4; ++i)
+                    *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + FPT * qt + 4 * i) =
                         f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
             }
             // projection (models.py:206-212) -> grid_sample coords (encoder.py:95-108)
@@ -595,11 +622,11 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
                 __syncthreads();
                 PT(gc, 3);
                 // z = bilinear latent gather (torch's nw, ne, sw, se summation order).
-                // Wave w walks its 16 columns; each load instruction reads one contiguous
-                // 1 KB half of a corner's 2 KB channel row (lane = 4 channels).
+                // Wave w walks its COLS / WAVES columns; each load instruction reads one
+                // contiguous 1 KB half of a corner's 2 KB channel row (lane = 4 channels).
 #pragma unroll 4
-                for (int j = 0; j < 16; ++j) {
-                    const int cj = 16 * wave + j;
+                for (int j = 0; j < COLS / WAVES; ++j) {
+                    const int cj = (COLS / WAVES) * wave + j;
                     const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
                     const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
 #pragma unroll
@@ -682,12 +709,12 @@ __global__ __launch_bounds__(256, 1) void k_point_mlp(Args a) {
             add_bias(x, bias + (2 + l0) * H, wave, g, true);
             layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc);
         }
-        // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w -> columns 16w..
+        // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         __syncthreads();
         store_relu(x, inbuf, wave, lane);
         __syncthreads();
         PT(gc, 3);
-        {
+        if (wave < CT) {   // wave-uniform: the first CT waves own one column tile each
             const float *wo = a.packed + L.off_lin_out + lane * 4;
             const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
             f4 o0 = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * g);
@@ -824,13 +851,13 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
                                         mlpk::COLS * 8);
     switch (d.precision) {
     case PNR_PREC_BF16X6:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<6>, dim3((unsigned)grid), dim3(256), lds, st, a);
+        hipLaunchKernelGGL(mlpk::k_point_mlp<6>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
         break;
     case PNR_PREC_BF16X9:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<9>, dim3((unsigned)grid), dim3(256), lds, st, a);
+        hipLaunchKernelGGL(mlpk::k_point_mlp<9>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
         break;
     default:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<0>, dim3((unsigned)grid), dim3(256), lds, st, a);
+        hipLaunchKernelGGL(mlpk::k_point_mlp<0>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
     }
     return launch_ok("point_mlp") ? PNR_OK : PNR_ERR_HIP;
 }
