@@ -46,7 +46,8 @@ MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
 MFMA_BF16_PEAK_TFLOPS = 2500.0 # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
 # fp32-equivalent peak of each ResnetFC arithmetic mode (pnr.models.PRECISIONS): the
 # split modes issue 6 / 9 bf16 MFMA products per fp32 multiply-add
-PEAK_BY_PRECISION = {"fp32": (MFMA_F32_PEAK_TFLOPS, 1), "bf16x6": (MFMA_BF16_PEAK_TFLOPS / 6, 6),
+PEAK_BY_PRECISION = {"fp32": (MFMA_F32_PEAK_TFLOPS, 1), "f16x3": (MFMA_BF16_PEAK_TFLOPS / 3, 3),
+                     "bf16x6": (MFMA_BF16_PEAK_TFLOPS / 6, 6),
                      "bf16x9": (MFMA_BF16_PEAK_TFLOPS / 9, 9)}
 ARITHMETIC = {
     "fp32": "v_mfma_f32_16x16x4_f32 (fp32 products, fp32 accumulate)",
@@ -54,6 +55,9 @@ ARITHMETIC = {
               "v_mfma_f32_16x16x32_bf16, fp32 accumulate (error at fp32 unit roundoff; "
               "profiles/r1/precision_study.json)",
     "bf16x9": "exact 3-way bf16 split, all 9 products (exact), fp32 accumulate",
+    "f16x3": "power-of-two scaled operands split into two fp16 parts, 3 exact products on "
+             "v_mfma_f32_16x16x32_f16 (f16 MFMA rate = bf16 rate), fp32 accumulate "
+             "(error at the fp32 level; profiles/*/precision_study.json)",
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOP_PER_POINT_NS1 = 4761600 + 2101248   # NS*4,761,600 + 2,101,248
@@ -193,7 +197,7 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-composite", action="store_true")
-    ap.add_argument("--precision", default="bf16x6", choices=sorted(PEAK_BY_PRECISION))
+    ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
     args = ap.parse_args()
 
     rank, world, local = pdist.init_from_env("nccl")   # RCCL on ROCm; control plane only

@@ -72,8 +72,14 @@ typedef struct pnr_mlp_desc {
  *                   all 9 part-products on v_mfma_f32_16x16x32_bf16: every product exact,
  *                   only the fp32 accumulation rounds (numerically an fp32 GEMM).
  *   PNR_PREC_BF16X6 the 6 largest of those products (drops x1*y2, x2*y1, x2*y2, each
- *                   < 2^-24 |x y|): error at the fp32 unit roundoff. */
+ *                   < 2^-24 |x y|): error at the fp32 unit roundoff.
+ *   PNR_PREC_F16X3  W (per layer) and every activation column scaled by a power of two
+ *                   (max <= 2^14), each split into two fp16 parts x = x0 + x1 (|x - x0 - x1|
+ *                   <= 2^-22 |x|); 3 exact products x0 y0 + x0 y1 + x1 y0 on
+ *                   v_mfma_f32_16x16x32_f16, fp32 accumulation, scales undone exactly.
+ *                   Error at the fp32 level (scripts/precision_study.py). */
 #define PNR_PREC_F32 0
+#define PNR_PREC_F16X3 3
 #define PNR_PREC_BF16X6 6
 #define PNR_PREC_BF16X9 9
 

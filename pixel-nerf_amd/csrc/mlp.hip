@@ -46,9 +46,15 @@ constexpr int KS32 = H / 32;       // 16 k-steps for K = 512
 constexpr int KS32_IN = 2;         // lin_in (d_in <= 64)
 constexpr int SRT_FLOATS = 768;    // one (k-step, row tile): 3 parts x 64 lanes x 8 bf16
 constexpr int SKS_FLOATS = NRT * SRT_FLOATS;  // one k-step of a packed layer (96 KB)
+// scaled-fp16 mode (PREC 3): 2 parts x 64 lanes x 8 f16 per (k-step, row tile)
+constexpr int SRT16_FLOATS = 512;
+constexpr int SKS16_FLOATS = NRT * SRT16_FLOATS;  // 64 KB
+constexpr int HDR_ESCALE = 32;     // header floats [32, 64): per-layer weight scale exponents
+                                   // (PREC 3): [32] lin_in, [33 + j] packed 512-wide layer j
+__host__ __device__ constexpr int sks_floats(int prec) { return prec == 3 ? SKS16_FLOATS : SKS_FLOATS; }
 
 struct Layout {
-    int prec;                      // 0 = f32 MFMA, 6 / 9 = split-bf16 products
+    int prec;                      // 0 = f32 MFMA, 6 / 9 = split-bf16 products, 3 = scaled f16
     int n_linz, n_l512, n_blocks, ncomb, d_in, d_out, pe_n;
     int64_t layer_floats;
     int64_t off_lin_in, off_l512, off_lin_out, off_bias, nbias, total;
@@ -64,9 +70,9 @@ inline Layout make_layout(const pnr_mlp_desc &d) {
     L.d_out = d.d_out;
     L.pe_n = d.pe_n;
     L.prec = d.precision;
-    L.layer_floats = L.prec ? (int64_t)KS32 * SKS_FLOATS : (int64_t)LAYER_FLOATS;
+    L.layer_floats = L.prec ? (int64_t)KS32 * sks_floats(L.prec) : (int64_t)LAYER_FLOATS;
     L.off_lin_in = HDR;
-    L.off_l512 = L.off_lin_in + (L.prec ? (int64_t)KS32_IN * SKS_FLOATS : (int64_t)NKB_IN * KB_FLOATS);
+    L.off_l512 = L.off_lin_in + (L.prec ? (int64_t)KS32_IN * sks_floats(L.prec) : (int64_t)NKB_IN * KB_FLOATS);
     L.off_lin_out = L.off_l512 + (int64_t)L.n_l512 * L.layer_floats;
     L.off_bias = L.off_lin_out + (int64_t)NKB * 256;
     L.nbias = (int64_t)(1 + L.n_l512) * H + 16;
@@ -92,6 +98,7 @@ __global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
     if (i >= L.total) return;
     float v = 0.0f;
     if (i < HDR) {
+        if (i >= HDR_ESCALE && L.prec == 3) return;   // written by k_layer_escale
         if (i < 16 && i < L.pe_n) v = s.pe_f[i];
         else if (i >= 16 && i < 32 && (i - 16) < L.pe_n) v = s.pe_p[i - 16];
     } else if (i < L.off_lin_out && L.prec) {
@@ -171,6 +178,70 @@ __global__ void k_pack_split(PackSrc s, Layout L, float *__restrict__ out) {
         v.x = p[q][0] | ((unsigned)p[q][1] << 16); v.y = p[q][2] | ((unsigned)p[q][3] << 16);
         v.z = p[q][4] | ((unsigned)p[q][5] << 16); v.w = p[q][6] | ((unsigned)p[q][7] << 16);
         *reinterpret_cast<uint4 *>(dst + q * 256) = v;
+    }
+}
+
+// Scaled-fp16 mode: per packed layer, the power-of-two exponent eW with
+// max|W| * 2^eW <= 2^14 (fp16 max 65504), clamped to [-64, 40].  One block per layer
+// (layer -1 = lin_in), written to the pack header as a float.
+__device__ __forceinline__ int scale_exp(float m) {
+    if (!(m > 0.f) || !(m < 3.0e38f)) return 0;       // zero / inf / nan: unscaled
+    int e = 14 - __builtin_amdgcn_frexp_expf(m);      // m < 2^frexp_exp
+    return e < -64 ? -64 : (e > 40 ? 40 : e);
+}
+__global__ void k_layer_escale(PackSrc s, Layout L, float *__restrict__ out) {
+    const int layer = (int)blockIdx.x - 1;
+    const float *w = layer < 0 ? s.lin_in_w : s.w[layer];
+    const int64_t n = layer < 0 ? (int64_t)H * L.d_in : (int64_t)H * H;
+    float m = 0.f;
+    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    m = wave_max(m);
+    __shared__ float red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        out[HDR_ESCALE + 1 + layer] = (float)scale_exp(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// One thread per (layer, k-step, row tile, lane): 8 weights w * 2^eW, each split
+// into two fp16 parts w0 = f16(w), w1 = f16(w - w0) (RNE), [ks][rt][part][lane][8].
+__global__ void k_pack_f16(PackSrc s, Layout L, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n_in = (int64_t)KS32_IN * NRT * 64;
+    const int64_t n_l = (int64_t)KS32 * NRT * 64;
+    if (t >= n_in + L.n_l512 * n_l) return;
+    int layer, ks, rt, lane;
+    float *dst;
+    if (t < n_in) {
+        layer = -1;
+        ks = (int)(t / (NRT * 64)); rt = (int)((t / 64) % NRT); lane = (int)(t % 64);
+        dst = out + L.off_lin_in + (int64_t)ks * SKS16_FLOATS + rt * SRT16_FLOATS + lane * 4;
+    } else {
+        const int64_t r = t - n_in;
+        layer = (int)(r / n_l);
+        const int64_t e = r % n_l;
+        ks = (int)(e / (NRT * 64)); rt = (int)((e / 64) % NRT); lane = (int)(e % 64);
+        dst = out + L.off_l512 + layer * L.layer_floats + (int64_t)ks * SKS16_FLOATS + rt * SRT16_FLOATS + lane * 4;
+    }
+    const int ew = (int)out[HDR_ESCALE + 1 + layer];
+    const int row = 16 * rt + (lane & 15);
+    _Float16 p[2][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int col = 32 * ks + 8 * (lane >> 4) + j;
+        float w = 0.f;
+        if (layer < 0) { if (col < L.d_in) w = s.lin_in_w[(int64_t)row * L.d_in + col]; }
+        else w = s.w[layer][(int64_t)row * H + col];
+        const float ws = __builtin_ldexpf(w, ew);
+        const _Float16 h0 = (_Float16)ws;
+        p[0][j] = h0;
+        p[1][j] = (_Float16)(ws - (float)h0);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        typedef _Float16 h8t __attribute__((ext_vector_type(8)));
+        h8t v = {p[q][0], p[q][1], p[q][2], p[q][3], p[q][4], p[q][5], p[q][6], p[q][7]};
+        *reinterpret_cast<h8t *>(dst + q * 256) = v;
     }
 }
 
@@ -401,6 +472,95 @@ __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ w
     }
 }
 
+// ---- scaled-fp16 mode (PREC 3) -----------------------------------------------------
+// W * 2^eW and every IN column * 2^e_col are split exactly enough into two fp16 parts
+// (x = x0 + x1 + O(2^-22 x)); three products x0 y0 + x0 y1 + x1 y0 are exact in the
+// f32 accumulate of v_mfma_f32_16x16x32_f16 (dropped x1 y1 < 2^-22 |x y|).  The
+// power-of-two scales keep both operands in fp16's normal range (max <= 2^14) and are
+// undone exactly on the fp32 accumulators.
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+constexpr int STG16_FLOATS = CT * 2 * 256;   // one staging buffer: [ct][part][lane][8 f16]
+
+__device__ __forceinline__ f4 mfma_h(h8 a, h8 b, f4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// 4 values * s -> packed fp16 parts (2 dwords each): v_cvt_pk_f16_f32 (RNE), back, subtract
+__device__ __forceinline__ void split_f16x4(const f4 &v, float s, u2 &p0, u2 &p1) {
+    const f2 a = {v.x * s, v.y * s}, b = {v.z * s, v.w * s};
+    const h2 a0 = __builtin_convertvector(a, h2), b0 = __builtin_convertvector(b, h2);
+    const f2 ar = a - __builtin_convertvector(a0, f2), br = b - __builtin_convertvector(b0, f2);
+    const h2 a1 = __builtin_convertvector(ar, h2), b1 = __builtin_convertvector(br, h2);
+    p0 = u2{__builtin_bit_cast(unsigned, a0), __builtin_bit_cast(unsigned, b0)};
+    p1 = u2{__builtin_bit_cast(unsigned, a1), __builtin_bit_cast(unsigned, b1)};
+}
+
+// acc[r][c] += (W 2^eW)(IN 2^e) over NKS k-steps of 32; same pipeline as gemm_split
+// (staging ring split by the waves, A ring A_DIST row tiles ahead).  s_split = 2^e of
+// the column this lane splits.
+template <int NKS>
+__device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const float *inbw,
+                                         float *stg, int wave, int lane, float s_split) {
+    h8 ra[A_RING][2];
+    auto loadA = [&](h8 (&dst)[2], int ks, int r) {
+        const float *src = wp + (int64_t)ks * SKS16_FLOATS + r * SRT16_FLOATS;
+        dst[0] = *reinterpret_cast<const h8 *>(src);
+        dst[1] = *reinterpret_cast<const h8 *>(src + 256);
+    };
+    auto split_own = [&](int ks, int buf) {
+        const float *bp = inbw + 32 * ks;
+        if constexpr (WAVES == 4) {
+            u2 l0, l1, h0, h1;
+            split_f16x4(*reinterpret_cast<const f4 *>(bp), s_split, l0, l1);
+            split_f16x4(*reinterpret_cast<const f4 *>(bp + 4), s_split, h0, h1);
+            float *d = stg + buf * STG16_FLOATS + wave * 512 + lane * 4;
+            *reinterpret_cast<u4 *>(d) = u4{l0.x, l0.y, h0.x, h0.y};
+            *reinterpret_cast<u4 *>(d + 256) = u4{l1.x, l1.y, h1.x, h1.y};
+        } else {
+            u2 p0, p1;
+            split_f16x4(*reinterpret_cast<const f4 *>(bp), s_split, p0, p1);
+            float *d = stg + buf * STG16_FLOATS + (wave % CT) * 512 + lane * 4 + 2 * (wave / CT);
+            *reinterpret_cast<u2 *>(d) = p0;
+            *reinterpret_cast<u2 *>(d + 256) = p1;
+        }
+    };
+    split_own(0, 0);
+#pragma unroll
+    for (int r = 0; r < A_DIST; ++r) loadA(ra[r], 0, r);
+    lds_barrier();
+#pragma unroll 1
+    for (int ks = 0; ks < NKS; ++ks) {
+        const int kn = ks + 1 < NKS ? ks + 1 : ks;
+        h8 b0[CT], b1[CT];
+        const float *sp = stg + (ks & 1) * STG16_FLOATS + lane * 4;
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            b0[c] = *reinterpret_cast<const h8 *>(sp + c * 512);
+            b1[c] = *reinterpret_cast<const h8 *>(sp + c * 512 + 256);
+        }
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            if (r == 1) split_own(kn, (ks + 1) & 1);
+            const int rn = r + A_DIST;
+            if (rn < RTW) loadA(ra[rn % A_RING], ks, rn);
+            else loadA(ra[rn % A_RING], kn, rn - RTW);
+            __builtin_amdgcn_sched_barrier(0);
+            const h8 *a = ra[r % A_RING];
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+                f4 v = acc[r][c];
+                v = mfma_h(a[1], b0[c], v);
+                v = mfma_h(a[0], b1[c], v);
+                v = mfma_h(a[0], b0[c], v);
+                acc[r][c] = v;
+            }
+        }
+        lds_barrier();
+    }
+}
+
 // acc = bias (per output row) [+ acc]
 __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bias, int wave, int g,
                                          bool accumulate) {
@@ -431,9 +591,15 @@ __device__ __forceinline__ void unpark(Acc &acc, const float *xp) {
         for (int c = 0; c < CT; ++c) acc[r][c] = *reinterpret_cast<const f4 *>(xp + (r * CT + c) * 256);
 }
 
-// IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane)
-__device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wave, int lane) {
+// IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane).
+// kMax (PREC 3): also this wave's per-column maximum -> cmax[column][wave slot].
+template <bool kMax = false>
+__device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wave, int lane,
+                                           float *cmax = nullptr) {
     const int g = lane >> 4, cl = lane & 15;
+    float m[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) m[c] = 0.f;
 #pragma unroll
     for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -441,7 +607,19 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
             const f4 v = acc[r][c];
             f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
             *reinterpret_cast<f4 *>(inbuf + (16 * c + cl) * LDS_LD + 16 * (RTW * wave + r) + 4 * g) = o;
+            if constexpr (kMax) m[c] = fmaxf(fmaxf(m[c], fmaxf(o.x, o.y)), fmaxf(o.z, o.w));
         }
+    if constexpr (kMax) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            float v = fmaxf(m[c], __shfl_xor(m[c], 16, 64));
+            v = fmaxf(v, __shfl_xor(v, 32, 64));
+            if (g == 0) {
+                cmax[(16 * c + cl) * 8 + wave] = v;
+                if constexpr (WAVES == 4) cmax[(16 * c + cl) * 8 + wave + 4] = v;
+            }
+        }
+    }
 }
 
 // Diagnostic build only (-DPNR_PHASE_TIMING, scripts/build_variant.sh): wave-0 shader
@@ -466,18 +644,52 @@ struct GemmCtx {
     const float *inb4;        // f32 B: column 16c + cl, k 16kb + 4g
     const float *inbw;        // split: own column tile 16*wave + cl, k 8g
     float *stg;               // split staging ring
+    const float *hdr;         // pack header (PREC 3 weight scale exponents)
+    const float *cmax;        // PREC 3: per-column partial maxima of IN, [64][8]
     int wave, lane;
 #ifdef PNR_PHASE_TIMING
     uint64_t pt[8], pt_last;
 #endif
 };
 
+// PREC 3: power-of-two scale exponent of IN column `col` from its partial maxima
+__device__ __forceinline__ int col_exp(const float *cmax, int col) {
+    const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
+    const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
+    const float m = fmaxf(fmaxf(fmaxf(m0.x, m0.y), fmaxf(m0.z, m0.w)), fmaxf(fmaxf(m1.x, m1.y), fmaxf(m1.z, m1.w)));
+    return scale_exp(m);
+}
+
+// hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index)
 template <int PREC, int NK>
-__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g) {
+__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx) {
     PT(g, 3);
     PT_COUNT(g, 5);
-    if constexpr (PREC == 0) gemm<NK>(acc, layer_base + g.wl_off, g.inb4);
-    else gemm_split<NK / 2, PREC>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane);
+    if constexpr (PREC == 0) {
+        gemm<NK>(acc, layer_base + g.wl_off, g.inb4);
+    } else if constexpr (PREC == 3) {
+        const int cl = g.lane & 15;
+        const int ew = (int)g.hdr[HDR_ESCALE + hidx];
+        float sa[CT], ia[CT];
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const int e = col_exp(g.cmax, 16 * c + cl) + ew;
+            sa[c] = __builtin_ldexpf(1.f, e);
+            ia[c] = __builtin_ldexpf(1.f, -e);
+        }
+        const float s_split = __builtin_ldexpf(1.f, col_exp(g.cmax, 16 * (g.wave % CT) + cl));
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+#pragma unroll
+            for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
+        gemm_f16<NK / 2>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane, s_split);
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+#pragma unroll
+            for (int c = 0; c < CT; ++c) acc[r][c] *= ia[c];
+    } else {
+        gemm_split<NK / 2, PREC>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane);
+    }
     PT(g, 2);
 }
 
@@ -497,7 +709,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 
     // per-lane fragment bases
     const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;         // f32 fragments
-    const int64_t ws_off = (int64_t)(RTW * wave) * SRT_FLOATS + lane * 4;  // split fragments
+    const int64_t ws_off = (int64_t)(RTW * wave) * (PREC == 3 ? SRT16_FLOATS : SRT_FLOATS) + lane * 4;
     const float *inb = inbuf + cl * LDS_LD + 4 * g;     // B (f32): column 16c + cl, k 16kb + 4g
     GemmCtx gc;
     gc.wl_off = wl_off;
@@ -506,6 +718,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.inbw = inbuf + (16 * (wave % CT) + cl) * LDS_LD + 8 * g + 4 * (wave / CT);
     gc.stg = inbuf + COLS * LDS_LD;
     float *gtab = gc.stg + 2 * STG_FLOATS;   // per-column gather records (64 x 8 floats)
+    float *cmax = gtab + COLS * 8;           // PREC 3: per-column partial maxima (64 x 8)
+    gc.hdr = a.packed;
+    gc.cmax = cmax;
     gc.wave = wave;
     gc.lane = lane;
 #ifdef PNR_PHASE_TIMING
@@ -578,6 +793,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 for (int i = 0; i < FPT / 4; ++i)
                     *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + FPT * qt + 4 * i) =
                         f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
+                if constexpr (PREC == 3) {
+                    float m = 0.f;
+#pragma unroll
+                    for (int i = 0; i < FPT; ++i) m = fmaxf(m, fabsf(fv[i]));
+                    cmax[col * 8 + qt] = m;
+                    if constexpr (WAVES == 4) cmax[col * 8 + qt + 4] = m;
+                }
             }
             // projection (models.py:206-212) -> grid_sample coords (encoder.py:95-108)
             float u = mul_rn(__fdiv_rn(-xc[0], xc[2]), fx);
@@ -615,7 +837,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, g, false);
-            layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, gc);
+            layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, gc, 0);
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
@@ -628,6 +850,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 for (int j = 0; j < COLS / WAVES; ++j) {
                     const int cj = (COLS / WAVES) * wave + j;
                     const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
+                    float zmax = 0.f;
                     const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
 #pragma unroll
                     for (int half = 0; half < 2; ++half) {
@@ -646,24 +869,33 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                             zz[q] = add_rn(add_rn(add_rn(mul_rn(c0[q], tw.x), mul_rn(c1[q], tw.y)),
                                                   mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
                         *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
+                        if constexpr (PREC == 3)
+                            zmax = fmaxf(zmax, fmaxf(fmaxf(fabsf(zz[0]), fabsf(zz[1])),
+                                                     fmaxf(fabsf(zz[2]), fabsf(zz[3]))));
+                    }
+                    if constexpr (PREC == 3) {
+                        zmax = fmaxf(zmax, __shfl_xor(zmax, 8, 64));
+                        zmax = fmaxf(zmax, __shfl_xor(zmax, 16, 64));
+                        zmax = fmaxf(zmax, __shfl_xor(zmax, 32, 64));
+                        if (lane < 8) cmax[cj * 8 + lane] = zmax;
                     }
                 }
                 __syncthreads();
                 PT(gc, 1);
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
-                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc);
+                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 __syncthreads();
-                store_relu(x, inbuf, wave, lane);
+                store_relu<PREC == 3>(x, inbuf, wave, lane, cmax);
                 if constexpr (PREC != 0 && kParkX) park(x, xp);
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, g, false);
-                layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc);
+                layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
                 __syncthreads();
-                store_relu(h, inbuf, wave, lane);
+                store_relu<PREC == 3>(h, inbuf, wave, lane, cmax);
                 __syncthreads();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp);
                 add_bias(x, bias + (3 + lz) * H, wave, g, true);
-                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc);
+                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -697,17 +929,17 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             __syncthreads();
-            store_relu(x, inbuf, wave, lane);
+            store_relu<PREC == 3>(x, inbuf, wave, lane, cmax);
             if constexpr (PREC != 0 && kParkX) park(x, xp);
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, g, false);
-            layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc);
+            layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
             __syncthreads();
-            store_relu(h, inbuf, wave, lane);
+            store_relu<PREC == 3>(h, inbuf, wave, lane, cmax);
             __syncthreads();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp);
             add_bias(x, bias + (2 + l0) * H, wave, g, true);
-            layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc);
+            layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         __syncthreads();
@@ -780,8 +1012,10 @@ int mlp_check_desc(const pnr_mlp_desc &d) {
     if (d.d_in != 3 + 3 * d.pe_n + 3)
         return fail(PNR_ERR_UNSUPPORTED, "d_in must be 3 + 3*pe_n + 3 (xyz PE + raw viewdirs); got %d", d.d_in);
     if (d.d_in > 16 * mlpk::NKB_IN) return fail(PNR_ERR_UNSUPPORTED, "d_in <= 64");
-    if (d.precision != PNR_PREC_F32 && d.precision != PNR_PREC_BF16X6 && d.precision != PNR_PREC_BF16X9)
-        return fail(PNR_ERR_UNSUPPORTED, "precision must be 0 (f32), 6 or 9 (split bf16); got %d", d.precision);
+    if (d.precision != PNR_PREC_F32 && d.precision != PNR_PREC_F16X3 && d.precision != PNR_PREC_BF16X6 &&
+        d.precision != PNR_PREC_BF16X9)
+        return fail(PNR_ERR_UNSUPPORTED, "precision must be 0 (f32), 3 (scaled f16) or 6 / 9 (split bf16); got %d",
+                    d.precision);
     return PNR_OK;
 }
 
@@ -812,8 +1046,15 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
     hipLaunchKernelGGL(mlpk::k_pack, dim3((unsigned)blocks), dim3(256), 0, st, s, L,
                        static_cast<float *>(packed));
     if (!launch_ok("mlp_pack")) return PNR_ERR_HIP;
-    if (L.prec) {
-        const int64_t n = (int64_t)(mlpk::KS32_IN + L.n_l512 * mlpk::KS32) * mlpk::NRT * 64;
+    const int64_t n = (int64_t)(mlpk::KS32_IN + L.n_l512 * mlpk::KS32) * mlpk::NRT * 64;
+    if (L.prec == PNR_PREC_F16X3) {
+        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3((unsigned)(1 + L.n_l512)), dim3(256), 0, st, s, L,
+                           static_cast<float *>(packed));
+        if (!launch_ok("mlp_layer_escale")) return PNR_ERR_HIP;
+        hipLaunchKernelGGL(mlpk::k_pack_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                           s, L, static_cast<float *>(packed));
+        if (!launch_ok("mlp_pack_f16")) return PNR_ERR_HIP;
+    } else if (L.prec) {
         hipLaunchKernelGGL(mlpk::k_pack_split, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                            s, L, static_cast<float *>(packed));
         if (!launch_ok("mlp_pack_split")) return PNR_ERR_HIP;
@@ -847,9 +1088,13 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
+    // activations + staging ring + gather records + column maxima (PREC 3) = 160,768 B
     const size_t lds = sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS +
-                                        mlpk::COLS * 8);
+                                        2 * mlpk::COLS * 8);
     switch (d.precision) {
+    case PNR_PREC_F16X3:
+        hipLaunchKernelGGL(mlpk::k_point_mlp<3>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
+        break;
     case PNR_PREC_BF16X6:
         hipLaunchKernelGGL(mlpk::k_point_mlp<6>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
         break;

@@ -7,6 +7,6 @@ for round in 1 2; do
     lib=pixel-nerf_amd/build/$t/libpnr.so
     [ "$t" = default ] && lib=pixel-nerf_amd/pnr/libpnr.so
     timeout -k 10 180 env PNR_LIB_PATH=$lib N_CHUNKS=${N_CHUNKS:-10} COMPOSITE=${COMPOSITE:-} \
-      PREC=${PREC:-bf16x6} python scripts/mlp_probe.py || exit $?
+      PREC=${PREC:-f16x3} python scripts/mlp_probe.py || exit $?
   done
 done

@@ -9,7 +9,7 @@ import bench  # noqa: E402
 import torch  # noqa: E402
 from pnr.renderer import NeRFRenderer  # noqa: E402
 
-prec = os.environ.get("PREC", "bf16x6")
+prec = os.environ.get("PREC", "f16x3")
 n = int(os.environ.get("N_CHUNKS", "2"))
 dev = torch.device("cuda:0")
 sd, net, rays = bench.build_scene(dev, 0)

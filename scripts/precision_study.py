@@ -2,7 +2,7 @@
 """Accuracy and speed of the ResnetFC GEMM precision modes on one MI355X.
 
 For N random points of the SRN scene, compares the HIP point query in each mode
-("fp32" f32-MFMA, "bf16x9", "bf16x6" split-bf16 MFMA) and the CPU fp32 oracle
+("fp32" f32-MFMA, "bf16x9", "bf16x6" split-bf16 MFMA, "f16x3" scaled split-fp16) and the CPU fp32 oracle
 against an fp64 evaluation of the same network (oracle/ref_cpu.py in double),
 then times a cfg2 render chunk (4096 rays x (64 + 64)) per mode.
 Prints one JSON object.
@@ -69,7 +69,7 @@ def main():
     net.encode_latent(lat.to(dev), poses.to(dev), torch.tensor(131.25, device=dev), (128, 128))
     frame = util.gen_rays(synth.srn_poses([30.0]), 128, 128, torch.tensor(131.25), 0.01, 4.0)
     chunk = frame.reshape(-1, 8)[:4096].to(dev)[None]
-    for prec in ("fp32", "bf16x9", "bf16x6"):
+    for prec in ("fp32", "bf16x9", "bf16x6", "f16x3"):
         net.mlp_precision = prec
         with torch.no_grad():
             out = net(xyz.to(dev), coarse=True, viewdirs=vd.to(dev)).double().cpu()

@@ -1,0 +1,59 @@
+#!/usr/bin/env python
+"""Summarize a scripts/profile.sh run (gpurun_out/prof_<tag>) into profiles/<tag>/.
+
+  kernel_stats.csv  rocprofv3 --kernel-trace --stats summary (copied as is)
+  pmc_summary.csv   per-dispatch FETCH_SIZE / WRITE_SIZE (KB, as rocprofv3 reports them)
+                    and the HBM bytes with the gfx950 correction of MI355X_MICROARCH.md
+                    (FETCH_SIZE counts half of wide coalesced streaming reads: x2)
+
+Usage: python scripts/summarize_profile.py <tag> [note]
+"""
+import csv
+import os
+import shutil
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def read_counter(path):
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append(r)
+    return rows
+
+
+def main():
+    tag = sys.argv[1]
+    note = sys.argv[2] if len(sys.argv) > 2 else ""
+    src = os.path.join(REPO, "gpurun_out", "prof_" + tag)
+    dst = os.path.join(REPO, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    fetch = read_counter(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"))
+    write = read_counter(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"))
+    wmap = {r["Dispatch_Id"]: float(r["Counter_Value"]) for r in write}
+    lines = [
+        "# rocprofv3 PMC summary, %s (bench.py --steps 1 --warmup 0 --no-cpu) %s" % (tag, note),
+        "# FETCH_SIZE/WRITE_SIZE in KB as rocprofv3 reports them (per dispatch).",
+        "# gfx950: FETCH_SIZE reads 1/2 of wide coalesced streaming reads (MI355X_MICROARCH.md HBM)"
+        " -> corrected = 2x.",
+        "kernel,grid,dispatch_ms,FETCH_SIZE_KB,WRITE_SIZE_KB,hbm_bytes_corrected",
+    ]
+    for r in fetch:
+        name = r["Kernel_Name"].split("(")[0].strip()
+        if not name.startswith("pnr::"):
+            continue
+        fk = float(r["Counter_Value"])
+        wk = wmap.get(r["Dispatch_Id"], 0.0)
+        ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+        lines.append("%s,%s,%.4f,%.1f,%.1f,%d" % (name, r["Grid_Size"], ms, fk, wk,
+                                                  int((2 * fk + wk) * 1024)))
+    with open(os.path.join(dst, "pmc_summary.csv"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    print("wrote", dst)
+
+
+if __name__ == "__main__":
+    main()

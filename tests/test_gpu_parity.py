@@ -50,10 +50,10 @@ def model_conf(n_blocks=5, combine_layer=3):
                 mlp_fine=dict(mlp), encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
 
 
-PRECS = ["fp32", "bf16x6", "bf16x9"]
+PRECS = ["fp32", "f16x3", "bf16x6", "bf16x9"]
 
 
-def hip_net(cfg, arr, precision="bf16x6"):
+def hip_net(cfg, arr, precision="f16x3"):
     net = PixelNeRFNet(model_conf(cfg.get("n_blocks", 5), cfg.get("combine_layer", 3)))
     net.mlp_precision = precision
     if not cfg.get("with_fine", True):
@@ -70,7 +70,7 @@ def hip_net(cfg, arr, precision="bf16x6"):
     return net
 
 
-def hip_render(cfg, arr, want_weights=True, precision="bf16x6"):
+def hip_render(cfg, arr, want_weights=True, precision="f16x3"):
     net = hip_net(cfg, arr, precision)
     r = NeRFRenderer(n_coarse=cfg["n_coarse"], n_fine=cfg["n_fine"], n_fine_depth=cfg["n_fine_depth"],
                      depth_std=cfg["depth_std"], white_bkgd=cfg["white_bkgd"], lindisp=cfg["lindisp"])
@@ -196,6 +196,37 @@ def test_point_query_multiview_multiobject_vs_oracle(precision):
     with torch.no_grad():
         out = net(xyz.to(DEV), coarse=True, viewdirs=vd.to(DEV))
     assert_close(out, ref, "point query SB=2 NS=3")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
+@pytest.mark.parametrize("lat_scale,w_scale", [(1e-4, 1.0), (1e3, 1.0), (1.0, 1e-3), (0.0, 1.0)])
+def test_point_query_dynamic_range(precision, lat_scale, w_scale):
+    """Scaled-fp16 mode keeps fp32-level error when the latent / lin_z weights are far
+    from unit scale (per-column and per-layer power-of-two scaling), and on all-zero
+    latent columns.  Tolerance relative to the output's magnitude."""
+    sd = synth.pixelnerf_state(5)
+    for k in list(sd):
+        if ".lin_z." in k and k.endswith("weight"):
+            sd[k] = sd[k] * w_scale
+    lat = synth.latent(11, 1, 512, 16, 16) * lat_scale
+    poses = synth.srn_poses([10.0])
+    focal = torch.tensor(40.0)
+    xyz = torch.from_numpy(synth.hash_sym(91, (1, 300, 3), 0.5))
+    vd = torch.nn.functional.normalize(torch.from_numpy(synth.hash_sym(92, (1, 300, 3), 1.0)), dim=-1)
+    scene = ref_cpu.Scene(lat, poses, focal, 64, 64, None)
+    with torch.no_grad():
+        ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, True, vd)
+    net = PixelNeRFNet(model_conf())
+    net.mlp_precision = precision
+    net.load_state_dict(sd, strict=False)
+    net = net.to(DEV).eval()
+    net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (64, 64))
+    with torch.no_grad():
+        out = net(xyz.to(DEV), coarse=True, viewdirs=vd.to(DEV)).cpu()
+    mag = float(ref.abs().max())
+    assert torch.isfinite(out).all()
+    assert_close(out, ref, "dynamic range lat*%g w*%g" % (lat_scale, w_scale),
+                 atol=ATOL * max(1.0, mag))
 
 
 # ------------------------------------------------------------------ render --
