@@ -39,7 +39,7 @@ import torch.distributed as dist  # noqa: E402
 
 from pnr import _lib, synth, util  # noqa: E402
 from pnr import dist as pdist  # noqa: E402
-from pnr.models import PixelNeRFNet  # noqa: E402
+from pnr.models import PRECISIONS, PixelNeRFNet  # noqa: E402
 from pnr.renderer import NeRFRenderer  # noqa: E402
 
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
@@ -171,22 +171,23 @@ def composite_roofline(dev, ev):
     return res
 
 
-def pmc_traffic(kernel, pick):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary (rocprofv3
-    counters cannot be read live from inside the process)."""
+def pmc_traffic(kernel, render_pass):
+    """Mean HBM bytes per launch of `kernel` in `render_pass` ("fine" / "coarse") from the
+    newest committed PMC summary that has it (rocprofv3 counters cannot be read live from
+    inside the process).  Returns (bytes, summary path) or (None, None)."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")))
-    if not files:
-        return None
-    vals = []
-    for line in open(files[-1]):
-        if line.startswith("#") or line.startswith("kernel,"):
-            continue
-        f = line.strip().split(",")
-        if kernel in f[0]:
-            vals.append(int(f[5]))
-    return pick(vals) if vals else None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")), reverse=True):
+        vals = []
+        for line in open(path):
+            if line.startswith("#") or line.startswith("kernel,"):
+                continue
+            f = line.strip().split(",")
+            if f[0].endswith(kernel) and len(f) > 6 and f[6] == render_pass:
+                vals.append(int(f[5]))
+        if vals:
+            return sum(vals) // len(vals), os.path.relpath(path, REPO)
+    return None, None
 
 
 def main():
@@ -197,6 +198,8 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-composite", action="store_true")
+    ap.add_argument("--no-compare", action="store_true",
+                    help="skip the f32-MFMA comparison frame (profiling runs)")
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
     args = ap.parse_args()
 
@@ -269,7 +272,7 @@ def main():
 
     # same frame with the plain f32-MFMA arithmetic, for comparison (N = 1 only)
     value_fp32 = None
-    if world == 1 and args.precision != "fp32":
+    if world == 1 and args.precision != "fp32" and not args.no_compare:
         net.mlp_precision = "fp32"
         with torch.no_grad():
             step()
@@ -281,6 +284,8 @@ def main():
             value_fp32 = round(2 * W * H / (time.perf_counter() - t2), 1)
         net.mlp_precision = args.precision
 
+    prec_code = PRECISIONS[args.precision]
+    traffic, traffic_src = pmc_traffic("k_point_mlp<%d>" % prec_code, "fine")
     rays_total = W * H * args.steps * world
     value = rays_total / elapsed
     out = {
@@ -309,10 +314,11 @@ def main():
                      "mfma_issue": {"tflops": round(achieved * terms, 1),
                                     "peak": MFMA_F32_PEAK_TFLOPS if terms == 1 else MFMA_BF16_PEAK_TFLOPS,
                                     "products_per_fma": terms},
-                     "traffic": pmc_traffic("k_point_mlp", max),
+                     "traffic": traffic,
                      "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
-                                       "bench (profiles/*/pmc_summary.csv, FETCH x2 gfx950 "
-                                       "correction)", "flop_per_launch": flop_fine,
+                                       "bench, fine-pass launches of k_point_mlp<%d> (%s, FETCH x2 "
+                                       "gfx950 correction)" % (prec_code, traffic_src),
+                     "flop_per_launch": flop_fine,
                      "launch_ms": round(avg["mlp_fine"], 4)},
         "kernel_ms": {n: round(v, 4) for n, v in avg.items()},
     }
