@@ -102,7 +102,9 @@ __global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
         if (i < 16 && i < L.pe_n) v = s.pe_f[i];
         else if (i >= 16 && i < 32 && (i - 16) < L.pe_n) v = s.pe_p[i - 16];
     } else if (i < L.off_lin_out && L.prec) {
-        return;   // written by k_pack_split
+        return;   // written by k_pack_split / k_pack_f16
+    } else if (i < L.off_bias && L.prec == 3) {
+        return;   // lin_out: written by k_pack_f16
     } else if (i < L.off_l512) {
         const int e = (int)(i - L.off_lin_in);
         const int kb = e / KB_FLOATS, rt = (e / 256) % NRT, lane = (e >> 2) & 63, j = e & 3;
@@ -183,7 +185,8 @@ __global__ void k_pack_split(PackSrc s, Layout L, float *__restrict__ out) {
 
 // Scaled-fp16 mode: per packed layer, the power-of-two exponent eW with
 // max|W| * 2^eW <= 2^14 (fp16 max 65504), clamped to [-64, 40].  One block per layer
-// (layer -1 = lin_in), written to the pack header as a float.
+// (block 0 = lin_in, 1 + j = packed 512-wide layer j, 1 + n_l512 = lin_out), written
+// to the pack header slot HDR_ESCALE + block as a float.
 __device__ __forceinline__ int scale_exp(float m) {
     if (!(m > 0.f) || !(m < 3.0e38f)) return 0;       // zero / inf / nan: unscaled
     int e = 14 - __builtin_amdgcn_frexp_expf(m);      // m < 2^frexp_exp
@@ -191,8 +194,9 @@ __device__ __forceinline__ int scale_exp(float m) {
 }
 __global__ void k_layer_escale(PackSrc s, Layout L, float *__restrict__ out) {
     const int layer = (int)blockIdx.x - 1;
-    const float *w = layer < 0 ? s.lin_in_w : s.w[layer];
-    const int64_t n = layer < 0 ? (int64_t)H * L.d_in : (int64_t)H * H;
+    const bool out_layer = layer == L.n_l512;
+    const float *w = layer < 0 ? s.lin_in_w : (out_layer ? s.lin_out_w : s.w[layer]);
+    const int64_t n = layer < 0 ? (int64_t)H * L.d_in : (out_layer ? (int64_t)L.d_out * H : (int64_t)H * H);
     float m = 0.f;
     for (int64_t i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
     m = wave_max(m);
@@ -205,14 +209,20 @@ __global__ void k_layer_escale(PackSrc s, Layout L, float *__restrict__ out) {
 
 // One thread per (layer, k-step, row tile, lane): 8 weights w * 2^eW, each split
 // into two fp16 parts w0 = f16(w), w1 = f16(w - w0) (RNE), [ks][rt][part][lane][8].
+// lin_out (rows padded to 16): [ks][part][lane][8].
 __global__ void k_pack_f16(PackSrc s, Layout L, float *__restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n_in = (int64_t)KS32_IN * NRT * 64;
     const int64_t n_l = (int64_t)KS32 * NRT * 64;
-    if (t >= n_in + L.n_l512 * n_l) return;
+    const int64_t n_all = n_in + L.n_l512 * n_l;
+    if (t >= n_all + KS32 * 64) return;
     int layer, ks, rt, lane;
     float *dst;
-    if (t < n_in) {
+    if (t >= n_all) {
+        layer = L.n_l512;   // lin_out
+        ks = (int)((t - n_all) / 64); rt = 0; lane = (int)((t - n_all) % 64);
+        dst = out + L.off_lin_out + ks * 512 + lane * 4;
+    } else if (t < n_in) {
         layer = -1;
         ks = (int)(t / (NRT * 64)); rt = (int)((t / 64) % NRT); lane = (int)(t % 64);
         dst = out + L.off_lin_in + (int64_t)ks * SKS16_FLOATS + rt * SRT16_FLOATS + lane * 4;
@@ -231,6 +241,7 @@ __global__ void k_pack_f16(PackSrc s, Layout L, float *__restrict__ out) {
         const int col = 32 * ks + 8 * (lane >> 4) + j;
         float w = 0.f;
         if (layer < 0) { if (col < L.d_in) w = s.lin_in_w[(int64_t)row * L.d_in + col]; }
+        else if (layer == L.n_l512) { if (row < L.d_out) w = s.lin_out_w[(int64_t)row * H + col]; }
         else w = s.w[layer][(int64_t)row * H + col];
         const float ws = __builtin_ldexpf(w, ew);
         const _Float16 h0 = (_Float16)ws;
@@ -482,7 +493,6 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef unsigned u2 __attribute__((ext_vector_type(2)));
-constexpr int STG16_FLOATS = CT * 2 * 256;   // one staging buffer: [ct][part][lane][8 f16]
 
 __device__ __forceinline__ f4 mfma_h(h8 a, h8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
@@ -497,55 +507,45 @@ __device__ __forceinline__ void split_f16x4(const f4 &v, float s, u2 &p0, u2 &p1
     p1 = u2{__builtin_bit_cast(unsigned, a1), __builtin_bit_cast(unsigned, b1)};
 }
 
-// acc[r][c] += (W 2^eW)(IN 2^e) over NKS k-steps of 32; same pipeline as gemm_split
-// (staging ring split by the waves, A ring A_DIST row tiles ahead).  s_split = 2^e of
-// the column this lane splits.
+// LDS image of the GEMM input in PREC 3: each activation column c scaled by 2^e_c and
+// split ONCE by its producer into two fp16 parts, P0 / P1 = [column][ROWH halves]
+// (4 B per element, the same as fp32).  The row pitch (1056 B = 66 x 16 B) makes the
+// B-fragment ds_read_b128 of every lane group hit 16 distinct 16-B bank quads.
+constexpr int ROWH = H + 16;                    // halves per column row
+constexpr int PART_HALVES = COLS * ROWH;        // one part (67,584 B)
+
+// acc[r][c] += (W 2^eW)(IN 2^e) over NKS k-steps of 32 from the pre-split LDS image:
+// no staging, no split, no barrier inside the layer (waves run free).  A fragments
+// stream from L2 A_DIST row tiles ahead; the last k-step is peeled so no load is in
+// flight when the accumulators are handed back.
+//   pb0 / pb1: P0 / P1 at (column cl, k 8g) of column tile 0
 template <int NKS>
-__device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const float *inbw,
-                                         float *stg, int wave, int lane, float s_split) {
+__device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
+                                         const _Float16 *pb1) {
     h8 ra[A_RING][2];
     auto loadA = [&](h8 (&dst)[2], int ks, int r) {
+#ifdef PNR_ABLATE_WSTREAM
+        ks = 0;  // diagnostic: no weight stream
+#endif
         const float *src = wp + (int64_t)ks * SKS16_FLOATS + r * SRT16_FLOATS;
         dst[0] = *reinterpret_cast<const h8 *>(src);
         dst[1] = *reinterpret_cast<const h8 *>(src + 256);
     };
-    auto split_own = [&](int ks, int buf) {
-        const float *bp = inbw + 32 * ks;
-        if constexpr (WAVES == 4) {
-            u2 l0, l1, h0, h1;
-            split_f16x4(*reinterpret_cast<const f4 *>(bp), s_split, l0, l1);
-            split_f16x4(*reinterpret_cast<const f4 *>(bp + 4), s_split, h0, h1);
-            float *d = stg + buf * STG16_FLOATS + wave * 512 + lane * 4;
-            *reinterpret_cast<u4 *>(d) = u4{l0.x, l0.y, h0.x, h0.y};
-            *reinterpret_cast<u4 *>(d + 256) = u4{l1.x, l1.y, h1.x, h1.y};
-        } else {
-            u2 p0, p1;
-            split_f16x4(*reinterpret_cast<const f4 *>(bp), s_split, p0, p1);
-            float *d = stg + buf * STG16_FLOATS + (wave % CT) * 512 + lane * 4 + 2 * (wave / CT);
-            *reinterpret_cast<u2 *>(d) = p0;
-            *reinterpret_cast<u2 *>(d + 256) = p1;
-        }
-    };
-    split_own(0, 0);
 #pragma unroll
     for (int r = 0; r < A_DIST; ++r) loadA(ra[r], 0, r);
-    lds_barrier();
-#pragma unroll 1
-    for (int ks = 0; ks < NKS; ++ks) {
-        const int kn = ks + 1 < NKS ? ks + 1 : ks;
+    auto kstep = [&](int ks, auto last_tag) {
+        constexpr bool last = decltype(last_tag)::value;
         h8 b0[CT], b1[CT];
-        const float *sp = stg + (ks & 1) * STG16_FLOATS + lane * 4;
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-            b0[c] = *reinterpret_cast<const h8 *>(sp + c * 512);
-            b1[c] = *reinterpret_cast<const h8 *>(sp + c * 512 + 256);
+            b0[c] = *reinterpret_cast<const h8 *>(pb0 + c * 16 * ROWH + 32 * ks);
+            b1[c] = *reinterpret_cast<const h8 *>(pb1 + c * 16 * ROWH + 32 * ks);
         }
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
-            if (r == 1) split_own(kn, (ks + 1) & 1);
             const int rn = r + A_DIST;
             if (rn < RTW) loadA(ra[rn % A_RING], ks, rn);
-            else loadA(ra[rn % A_RING], kn, rn - RTW);
+            else if (!last) loadA(ra[rn % A_RING], ks + 1, rn - RTW);
             __builtin_amdgcn_sched_barrier(0);
             const h8 *a = ra[r % A_RING];
 #pragma unroll
@@ -557,7 +557,60 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
                 acc[r][c] = v;
             }
         }
-        lds_barrier();
+    };
+#pragma unroll 1
+    for (int ks = 0; ks + 1 < NKS; ++ks) kstep(ks, std::false_type{});
+    kstep(NKS - 1, std::true_type{});
+}
+
+// 4 (or 8) fp32 values -> scaled fp16 parts written to P0 / P1 at half offset `off`
+__device__ __forceinline__ void put_split4(_Float16 *P0, _Float16 *P1, int off, const f4 &v, float s) {
+    u2 p0, p1;
+    split_f16x4(v, s, p0, p1);
+    *reinterpret_cast<u2 *>(P0 + off) = p0;
+    *reinterpret_cast<u2 *>(P1 + off) = p1;
+}
+
+// relu(acc) of this wave's rows -> per-column partial maxima cmax[column][wave slot]
+__device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        float m = 0.f;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            const f4 v = acc[r][c];
+            m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+        }
+        m = fmaxf(m, __shfl_xor(m, 16, 64));
+        m = fmaxf(m, __shfl_xor(m, 32, 64));
+        if (g == 0) {
+            cmax[(16 * c + cl) * 8 + wave] = m;
+            if constexpr (WAVES == 4) cmax[(16 * c + cl) * 8 + wave + 4] = m;
+        }
+    }
+}
+
+// after relu_colmax + barrier: relu(acc) * 2^e_col split into P0 / P1 (this wave's rows),
+// e_col -> ecol[column]
+__device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
+                                                 const float *cmax, int *ecol, int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int col = 16 * c + cl;
+        const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
+        const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
+        const int e = scale_exp(fmaxf(fmaxf(fmaxf(m0.x, m0.y), fmaxf(m0.z, m0.w)),
+                                      fmaxf(fmaxf(m1.x, m1.y), fmaxf(m1.z, m1.w))));
+        const float sc = __builtin_ldexpf(1.f, e);
+        if (wave == 0 && g == 0) ecol[col] = e;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            const f4 v = acc[r][c];
+            const f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+            put_split4(P0, P1, col * ROWH + 16 * (RTW * wave + r) + 4 * g, o, sc);
+        }
     }
 }
 
@@ -591,15 +644,9 @@ __device__ __forceinline__ void unpark(Acc &acc, const float *xp) {
         for (int c = 0; c < CT; ++c) acc[r][c] = *reinterpret_cast<const f4 *>(xp + (r * CT + c) * 256);
 }
 
-// IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane).
-// kMax (PREC 3): also this wave's per-column maximum -> cmax[column][wave slot].
-template <bool kMax = false>
-__device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wave, int lane,
-                                           float *cmax = nullptr) {
+// IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane)
+__device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wave, int lane) {
     const int g = lane >> 4, cl = lane & 15;
-    float m[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c) m[c] = 0.f;
 #pragma unroll
     for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -607,19 +654,7 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
             const f4 v = acc[r][c];
             f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
             *reinterpret_cast<f4 *>(inbuf + (16 * c + cl) * LDS_LD + 16 * (RTW * wave + r) + 4 * g) = o;
-            if constexpr (kMax) m[c] = fmaxf(fmaxf(m[c], fmaxf(o.x, o.y)), fmaxf(o.z, o.w));
         }
-    if constexpr (kMax) {
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            float v = fmaxf(m[c], __shfl_xor(m[c], 16, 64));
-            v = fmaxf(v, __shfl_xor(v, 32, 64));
-            if (g == 0) {
-                cmax[(16 * c + cl) * 8 + wave] = v;
-                if constexpr (WAVES == 4) cmax[(16 * c + cl) * 8 + wave + 4] = v;
-            }
-        }
-    }
 }
 
 // Diagnostic build only (-DPNR_PHASE_TIMING, scripts/build_variant.sh): wave-0 shader
@@ -645,20 +680,13 @@ struct GemmCtx {
     const float *inbw;        // split: own column tile 16*wave + cl, k 8g
     float *stg;               // split staging ring
     const float *hdr;         // pack header (PREC 3 weight scale exponents)
-    const float *cmax;        // PREC 3: per-column partial maxima of IN, [64][8]
+    const _Float16 *pb0, *pb1;  // PREC 3: P0 / P1 at (column cl, k 8g)
+    const int *ecol;          // PREC 3: scale exponent of each IN column
     int wave, lane;
 #ifdef PNR_PHASE_TIMING
     uint64_t pt[8], pt_last;
 #endif
 };
-
-// PREC 3: power-of-two scale exponent of IN column `col` from its partial maxima
-__device__ __forceinline__ int col_exp(const float *cmax, int col) {
-    const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
-    const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
-    const float m = fmaxf(fmaxf(fmaxf(m0.x, m0.y), fmaxf(m0.z, m0.w)), fmaxf(fmaxf(m1.x, m1.y), fmaxf(m1.z, m1.w)));
-    return scale_exp(m);
-}
 
 // hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index)
 template <int PREC, int NK>
@@ -668,21 +696,22 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
     if constexpr (PREC == 0) {
         gemm<NK>(acc, layer_base + g.wl_off, g.inb4);
     } else if constexpr (PREC == 3) {
+        // the accumulators run in the products' scale 2^(eW + e_col): exact for powers of
+        // two, so the fp32 rounding sequence is that of the unscaled sum
         const int cl = g.lane & 15;
         const int ew = (int)g.hdr[HDR_ESCALE + hidx];
         float sa[CT], ia[CT];
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-            const int e = col_exp(g.cmax, 16 * c + cl) + ew;
+            const int e = g.ecol[16 * c + cl] + ew;
             sa[c] = __builtin_ldexpf(1.f, e);
             ia[c] = __builtin_ldexpf(1.f, -e);
         }
-        const float s_split = __builtin_ldexpf(1.f, col_exp(g.cmax, 16 * (g.wave % CT) + cl));
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
-        gemm_f16<NK / 2>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane, s_split);
+        gemm_f16<NK / 2>(acc, layer_base + g.ws_off, g.pb0, g.pb1);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -717,10 +746,16 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.inb4 = inb;
     gc.inbw = inbuf + (16 * (wave % CT) + cl) * LDS_LD + 8 * g + 4 * (wave / CT);
     gc.stg = inbuf + COLS * LDS_LD;
-    float *gtab = gc.stg + 2 * STG_FLOATS;   // per-column gather records (64 x 8 floats)
+    // PREC 3 LDS: P0 | P1 | gtab | cmax | ecol; else: inbuf (fp32) | staging | gtab
+    _Float16 *P0 = reinterpret_cast<_Float16 *>(smem);
+    _Float16 *P1 = P0 + PART_HALVES;
+    float *gtab = PREC == 3 ? reinterpret_cast<float *>(P1 + PART_HALVES) : gc.stg + 2 * STG_FLOATS;
     float *cmax = gtab + COLS * 8;           // PREC 3: per-column partial maxima (64 x 8)
+    int *ecol = reinterpret_cast<int *>(cmax + COLS * 8);
     gc.hdr = a.packed;
-    gc.cmax = cmax;
+    gc.pb0 = P0 + cl * ROWH + 8 * g;
+    gc.pb1 = P1 + cl * ROWH + 8 * g;
+    gc.ecol = ecol;
     gc.wave = wave;
     gc.lane = lane;
 #ifdef PNR_PHASE_TIMING
@@ -730,6 +765,17 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // feature role: thread -> (column col, part qt of WAVES); FPT features each
     constexpr int FPT = 64 / WAVES;
     const int col = tid / WAVES, qt = tid % WAVES;
+
+    // relu(acc) -> the next GEMM's input image (callers barrier before and after)
+    auto publish_relu = [&](const Acc &acc) {
+        if constexpr (PREC == 3) {
+            relu_colmax(acc, cmax, wave, lane);
+            __syncthreads();
+            relu_store_split(acc, P0, P1, cmax, ecol, wave, lane);
+        } else {
+            store_relu(acc, inbuf, wave, lane);
+        }
+    };
 
     Acc x, h;
     for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
@@ -789,16 +835,25 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     }
                     fv[i] = val;
                 }
-#pragma unroll
-                for (int i = 0; i < FPT / 4; ++i)
-                    *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + FPT * qt + 4 * i) =
-                        f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
                 if constexpr (PREC == 3) {
+                    // column max over its WAVES feature threads (adjacent lanes), scale, split
                     float m = 0.f;
 #pragma unroll
                     for (int i = 0; i < FPT; ++i) m = fmaxf(m, fabsf(fv[i]));
-                    cmax[col * 8 + qt] = m;
-                    if constexpr (WAVES == 4) cmax[col * 8 + qt + 4] = m;
+#pragma unroll
+                    for (int o = 1; o < WAVES; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+                    const int e = scale_exp(m);
+                    const float sc = __builtin_ldexpf(1.f, e);
+#pragma unroll
+                    for (int i = 0; i < FPT / 4; ++i)
+                        put_split4(P0, P1, col * ROWH + FPT * qt + 4 * i,
+                                   f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]}, sc);
+                    if (qt == 0) ecol[col] = e;
+                } else {
+#pragma unroll
+                    for (int i = 0; i < FPT / 4; ++i)
+                        *reinterpret_cast<f4 *>(inbuf + col * LDS_LD + FPT * qt + 4 * i) =
+                            f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
                 }
             }
             // projection (models.py:206-212) -> grid_sample coords (encoder.py:95-108)
@@ -850,8 +905,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 for (int j = 0; j < COLS / WAVES; ++j) {
                     const int cj = (COLS / WAVES) * wave + j;
                     const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
-                    float zmax = 0.f;
                     const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
+                    f4 zh[2];
 #pragma unroll
                     for (int half = 0; half < 2; ++half) {
                         const uint32_t ch = half * 256 + lane * 4;
@@ -868,16 +923,22 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                         for (int q = 0; q < 4; ++q)
                             zz[q] = add_rn(add_rn(add_rn(mul_rn(c0[q], tw.x), mul_rn(c1[q], tw.y)),
                                                   mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
-                        *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
-                        if constexpr (PREC == 3)
-                            zmax = fmaxf(zmax, fmaxf(fmaxf(fabsf(zz[0]), fabsf(zz[1])),
-                                                     fmaxf(fabsf(zz[2]), fabsf(zz[3]))));
+                        if constexpr (PREC == 3) zh[half] = zz;
+                        else *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
                     }
                     if constexpr (PREC == 3) {
-                        zmax = fmaxf(zmax, __shfl_xor(zmax, 8, 64));
-                        zmax = fmaxf(zmax, __shfl_xor(zmax, 16, 64));
-                        zmax = fmaxf(zmax, __shfl_xor(zmax, 32, 64));
-                        if (lane < 8) cmax[cj * 8 + lane] = zmax;
+                        // column max over the wave (all 512 channels), scale, split
+                        float m = 0.f;
+#pragma unroll
+                        for (int hf = 0; hf < 2; ++hf)
+                            m = fmaxf(m, fmaxf(fmaxf(fabsf(zh[hf][0]), fabsf(zh[hf][1])),
+                                               fmaxf(fabsf(zh[hf][2]), fabsf(zh[hf][3]))));
+                        m = wave_max(m);
+                        const int e = scale_exp(m);
+                        const float sc = __builtin_ldexpf(1.f, e);
+                        put_split4(P0, P1, cj * ROWH + lane * 4, zh[0], sc);
+                        put_split4(P0, P1, cj * ROWH + 256 + lane * 4, zh[1], sc);
+                        if (lane == 0) ecol[cj] = e;
                     }
                 }
                 __syncthreads();
@@ -885,13 +946,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 __syncthreads();
-                store_relu<PREC == 3>(x, inbuf, wave, lane, cmax);
+                publish_relu(x);
                 if constexpr (PREC != 0 && kParkX) park(x, xp);
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, g, false);
                 layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
                 __syncthreads();
-                store_relu<PREC == 3>(h, inbuf, wave, lane, cmax);
+                publish_relu(h);
                 __syncthreads();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp);
                 add_bias(x, bias + (3 + lz) * H, wave, g, true);
@@ -929,13 +990,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             __syncthreads();
-            store_relu<PREC == 3>(x, inbuf, wave, lane, cmax);
+            publish_relu(x);
             if constexpr (PREC != 0 && kParkX) park(x, xp);
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, g, false);
             layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
             __syncthreads();
-            store_relu<PREC == 3>(h, inbuf, wave, lane, cmax);
+            publish_relu(h);
             __syncthreads();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp);
             add_bias(x, bias + (2 + l0) * H, wave, g, true);
@@ -943,10 +1004,44 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         __syncthreads();
-        store_relu(x, inbuf, wave, lane);
+        publish_relu(x);
         __syncthreads();
         PT(gc, 3);
-        if (wave < CT) {   // wave-uniform: the first CT waves own one column tile each
+        if (PREC == 3 && wave < CT) {
+            // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col
+            const float *wo = a.packed + L.off_lin_out + lane * 4;
+            const _Float16 *q0 = gc.pb0 + wave * 16 * ROWH, *q1 = gc.pb1 + wave * 16 * ROWH;
+            f4 o = {0.f, 0.f, 0.f, 0.f}, o2 = o;
+#pragma unroll 4
+            for (int ks = 0; ks < KS32; ks += 2) {
+                const h8 w0 = *reinterpret_cast<const h8 *>(wo + ks * 512);
+                const h8 w1 = *reinterpret_cast<const h8 *>(wo + ks * 512 + 256);
+                const h8 v0 = *reinterpret_cast<const h8 *>(q0 + 32 * ks);
+                const h8 v1 = *reinterpret_cast<const h8 *>(q1 + 32 * ks);
+                const h8 w2 = *reinterpret_cast<const h8 *>(wo + (ks + 1) * 512);
+                const h8 w3 = *reinterpret_cast<const h8 *>(wo + (ks + 1) * 512 + 256);
+                const h8 v2 = *reinterpret_cast<const h8 *>(q0 + 32 * (ks + 1));
+                const h8 v3 = *reinterpret_cast<const h8 *>(q1 + 32 * (ks + 1));
+                o = mfma_h(w1, v0, o);
+                o2 = mfma_h(w3, v2, o2);
+                o = mfma_h(w0, v1, o);
+                o2 = mfma_h(w2, v3, o2);
+                o = mfma_h(w0, v0, o);
+                o2 = mfma_h(w2, v2, o2);
+            }
+            const int e = ecol[16 * wave + cl] + (int)a.packed[HDR_ESCALE + 1 + L.n_l512];
+            const f4 b = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * g);
+            o = (o + o2) * __builtin_ldexpf(1.f, -e) + b;
+            const int64_t po = tile * COLS + 16 * wave + cl;
+            if (g == 0 && po < a.n_points) {
+                f4 r;
+                r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
+                r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
+                r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
+                r.w = fmaxf(o.w, 0.f);
+                *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+            }
+        } else if (PREC != 3 && wave < CT) {   // wave-uniform: the first CT waves own one column tile each
             const float *wo = a.packed + L.off_lin_out + lane * 4;
             const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
             f4 o0 = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * g);
@@ -1048,10 +1143,10 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
     if (!launch_ok("mlp_pack")) return PNR_ERR_HIP;
     const int64_t n = (int64_t)(mlpk::KS32_IN + L.n_l512 * mlpk::KS32) * mlpk::NRT * 64;
     if (L.prec == PNR_PREC_F16X3) {
-        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3((unsigned)(1 + L.n_l512)), dim3(256), 0, st, s, L,
+        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3((unsigned)(2 + L.n_l512)), dim3(256), 0, st, s, L,
                            static_cast<float *>(packed));
         if (!launch_ok("mlp_layer_escale")) return PNR_ERR_HIP;
-        hipLaunchKernelGGL(mlpk::k_pack_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(mlpk::k_pack_f16, dim3((unsigned)((n + mlpk::KS32 * 64 + 255) / 256)), dim3(256), 0, st,
                            s, L, static_cast<float *>(packed));
         if (!launch_ok("mlp_pack_f16")) return PNR_ERR_HIP;
     } else if (L.prec) {
@@ -1088,9 +1183,11 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
-    // activations + staging ring + gather records + column maxima (PREC 3) = 160,768 B
-    const size_t lds = sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS +
-                                        2 * mlpk::COLS * 8);
+    // PREC 3: split image P0 + P1, gather records, column maxima, exponents = 139,520 B
+    // else:   fp32 activations + staging ring + gather records            = 158,720 B
+    const size_t lds = d.precision == PNR_PREC_F16X3
+        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS)
+        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8);
     switch (d.precision) {
     case PNR_PREC_F16X3:
         hipLaunchKernelGGL(mlpk::k_point_mlp<3>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);

@@ -1,0 +1,79 @@
+#!/usr/bin/env python
+"""Derived PMC metrics of the k_point_mlp launches from scripts/counters.sh output.
+
+Usage: python scripts/analyze_counters.py gpurun_out/ctr_<tag>
+Per render pass (coarse / fine, told apart by launch order within each probe chunk:
+coarse MLP first, then fine) prints the mean over launches of:
+  clock_ghz      GRBM_GUI_ACTIVE / XCDs / duration
+  mfma_busy      SQ_VALU_MFMA_BUSY_CYCLES / (CUs * 4 SIMDs * clock cycles)
+  wait_any, wait_inst, active_inst   SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY
+                 as fractions of SQ_WAVE_CYCLES (MI355X_MICROARCH.md: disjoint, sum ~ 1)
+  lds_conflict   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
+  l2_hit         TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
+"""
+import csv
+import glob
+import os
+import sys
+from collections import defaultdict
+
+CUS, XCDS = 256, 8
+
+
+def load(d):
+    per = defaultdict(dict)   # dispatch id -> {counter: value, "name", "dur"}
+    for path in glob.glob(os.path.join(d, "g*", "run_counter_collection.csv")):
+        grp = os.path.basename(os.path.dirname(path))
+        with open(path) as f:
+            for r in csv.DictReader(f):
+                if "k_point_mlp" not in r["Kernel_Name"]:
+                    continue
+                key = (grp, int(r["Dispatch_Id"]))
+                e = per[key]
+                e["name"] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+                e["dur"] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+                e[r["Counter_Name"]] = float(r["Counter_Value"])
+    # label passes: within each group, MLP launches alternate coarse, fine (probe chunks)
+    out = defaultdict(lambda: defaultdict(list))
+    for grp in sorted(set(k[0] for k in per)):
+        ids = sorted(k[1] for k in per if k[0] == grp)
+        for i, did in enumerate(ids):
+            e = per[(grp, did)]
+            label = "%s %s" % (e["name"], "coarse" if i % 2 == 0 else "fine")
+            for k, v in e.items():
+                if k != "name":
+                    out[label][k].append(v)
+    return out
+
+
+def mean(v):
+    return sum(v) / len(v) if v else float("nan")
+
+
+def main():
+    res = load(sys.argv[1])
+    for label, c in sorted(res.items()):
+        m = {k: mean(v) for k, v in c.items()}
+        line = [label, "dur %.3f ms" % (m["dur"] * 1e3)]
+        if "GRBM_GUI_ACTIVE" in m:
+            clk = m["GRBM_GUI_ACTIVE"] / XCDS / m["dur"]
+            line.append("clock %.2f GHz" % (clk / 1e9))
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in m:
+                line.append("mfma_busy %.3f" % (m["SQ_VALU_MFMA_BUSY_CYCLES"] / (CUS * 4 * clk * m["dur"])))
+        if "SQ_WAVE_CYCLES" in m:
+            wc = m["SQ_WAVE_CYCLES"]
+            for k, nm in (("SQ_WAIT_ANY", "wait_any"), ("SQ_WAIT_INST_ANY", "wait_inst"),
+                          ("SQ_ACTIVE_INST_ANY", "active_inst")):
+                if k in m:
+                    line.append("%s %.3f" % (nm, m[k] / wc))
+        if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
+            line.append("lds_conflict %.3f" % (m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]))
+        if "TCC_HIT_sum" in m:
+            line.append("l2_hit %.4f" % (m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])))
+        if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
+            line.append("valu/mfma %.2f" % (m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"]))
+        print("  ".join(line))
+
+
+if __name__ == "__main__":
+    main()
