@@ -119,12 +119,90 @@ __global__ __launch_bounds__(64) void k_sample_fine(
 //   delta_i = z_{i+1} - z_i, delta_last = far - z_last
 //   alpha = 1 - exp(-delta * relu(sigma));  T = excl. cumprod(1 - alpha + 1e-10)
 //   w = alpha * T;  rgb = sum w c;  depth = sum w z;  white: rgb += 1 - sum w
-// One wave per ray, 4 rays per 256-thread block; the cumprod is a double-precision
-// wave scan (torch's CPU cumprod accumulates in double and rounds each prefix).
+// One wave per ray, 4 rays per 256-thread block; the cumprod accumulates in double
+// (torch's CPU cumprod accumulates in double and rounds each prefix).
 // ---------------------------------------------------------------------------
-// NCH > 0: K <= 64 NCH, every chunk's loads are issued before the first scan (more
-// bytes in flight per wave: the kernel is HBM-bound); NCH == 0: any K, chunk loop.
-template <int NCH>
+// S > 0 (K <= 64 S): lane l owns the S consecutive samples 64-lane-contiguous at S*l:
+// one sequential double product inside the lane, then ONE exclusive wave scan of the
+// lane products per ray; the next sample's z comes from the neighbour lane by shuffle.
+template <int S>
+__global__ __launch_bounds__(256) void k_composite_s(
+    const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
+    int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
+    float *__restrict__ rgb_out, float *__restrict__ depth_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= n_rays) return;
+    const float far = rays[b * 8 + 7];
+    const float *zr = z + b * K;
+    const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
+    const int k0 = S * lane;
+    float zk[S];
+    f4 v[S];
+    // unconditional (clamped) loads: all issue before the first wait
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const int kc = k0 + i < K ? k0 + i : K - 1;
+        zk[i] = __builtin_nontemporal_load(zr + kc);
+        v[i] = __builtin_nontemporal_load(rr + kc);
+    }
+    const float z_next_lane = dpp_f<0x130>(far, zk[0]);   // wave_shl:1 (lane + 1)
+    float alpha[S];
+    double lp[S + 1];   // exclusive in-lane prefix products
+    lp[0] = 1.0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const int k = k0 + i;
+        const bool valid = k < K;
+        const float zn = k + 1 >= K ? far : (i + 1 < S ? zk[i + 1] : z_next_lane);
+        const float delta = sub_rn(zn, zk[i]);
+        alpha[i] = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v[i].w, 0.0f)))) : 0.0f;
+        const float shifted = valid ? add_rn(sub_rn(1.0f, alpha[i]), 1e-10f) : 1.0f;
+        lp[i + 1] = lp[i] * (double)shifted;
+    }
+    const double excl = wave_shr1(wave_scan_mul(lp[S]), 1.0);   // product of earlier lanes
+    float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
+    float wk[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const bool valid = k0 + i < K;
+        wk[i] = valid ? mul_rn(alpha[i], (float)(excl * lp[i])) : 0.f;
+        sr += mul_rn(wk[i], v[i].x);
+        sg += mul_rn(wk[i], v[i].y);
+        sb += mul_rn(wk[i], v[i].z);
+        sd += mul_rn(wk[i], zk[i]);
+        sw += wk[i];
+    }
+    if (weights) {
+        float *wp = weights + b * K + k0;
+        if (S == 2 && (K & 1) == 0 && k0 < K) {   // 8-B aligned pair
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            __builtin_nontemporal_store(f2{wk[0], wk[1]}, reinterpret_cast<f2 *>(wp));
+        } else {
+#pragma unroll
+            for (int i = 0; i < S; ++i)
+                if (k0 + i < K) __builtin_nontemporal_store(wk[i], wp + i);
+        }
+    }
+    sr = wave_sum_dpp(sr);
+    sg = wave_sum_dpp(sg);
+    sb = wave_sum_dpp(sb);
+    sd = wave_sum_dpp(sd);
+    sw = wave_sum_dpp(sw);
+    if (lane == 0) {
+        if (white_bkgd) {
+            sr = sub_rn(add_rn(sr, 1.0f), sw);
+            sg = sub_rn(add_rn(sg, 1.0f), sw);
+            sb = sub_rn(add_rn(sb, 1.0f), sw);
+        }
+        rgb_out[b * 3 + 0] = sr;
+        rgb_out[b * 3 + 1] = sg;
+        rgb_out[b * 3 + 2] = sb;
+        depth_out[b] = sd;
+    }
+}
+
+// any K: 64-sample chunks, one wave scan per chunk with a running carry
 __global__ __launch_bounds__(256) void k_composite(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
     int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
@@ -135,60 +213,38 @@ __global__ __launch_bounds__(256) void k_composite(
     const float far = rays[b * 8 + 7];
     const float *zr = z + b * K;
     const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
-    constexpr int NR = NCH > 0 ? NCH : 1;
-    float zk[NR], zn[NR];
-    f4 v[NR];
-    auto load = [&](int i, int k) {
-        zk[i] = 0.f;
-        zn[i] = 0.f;
-        v[i] = f4{0.f, 0.f, 0.f, 0.f};
-        if (k < K) {
-            zk[i] = __builtin_nontemporal_load(zr + k);
-            zn[i] = (k + 1 < K) ? zr[k + 1] : far;
-            const float *rp = reinterpret_cast<const float *>(rr + k);
-            v[i] = f4{__builtin_nontemporal_load(rp), __builtin_nontemporal_load(rp + 1),
-                      __builtin_nontemporal_load(rp + 2), __builtin_nontemporal_load(rp + 3)};
-        }
-    };
-    if constexpr (NCH > 0) {
-#pragma unroll
-        for (int i = 0; i < NCH; ++i) load(i, 64 * i + lane);
-    }
     double carry = 1.0;
     float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
-    auto step = [&](int c, int i) {
-        const int k = 64 * c + lane;
+    for (int c0 = 0; c0 < K; c0 += 64) {
+        const int k = c0 + lane;
         const bool valid = k < K;
-        const float delta = sub_rn(zn[i], zk[i]);
-        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v[i].w, 0.0f)))) : 0.0f;
+        float zk = 0.f, zn = 0.f;
+        f4 v = {0.f, 0.f, 0.f, 0.f};
+        if (valid) {
+            zk = zr[k];
+            zn = (k + 1 < K) ? zr[k + 1] : far;
+            v = rr[k];
+        }
+        const float delta = sub_rn(zn, zk);
+        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v.w, 0.0f)))) : 0.0f;
         const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
-        double p = shifted;  // inclusive product scan
+        double p = shifted;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
-            double q = __shfl_up(p, off, 64);
+            const double q = __shfl_up(p, off, 64);
             if (lane >= off) p *= q;
         }
         double excl = __shfl_up(p, 1, 64);
         if (lane == 0) excl = 1.0;
-        const float T = (float)(carry * excl);
-        const float wk = mul_rn(alpha, T);
+        const float wk = mul_rn(alpha, (float)(carry * excl));
         carry *= __shfl(p, 63, 64);
         if (valid) {
-            if (weights) __builtin_nontemporal_store(wk, weights + b * K + k);
-            sr += mul_rn(wk, v[i].x);
-            sg += mul_rn(wk, v[i].y);
-            sb += mul_rn(wk, v[i].z);
-            sd += mul_rn(wk, zk[i]);
+            if (weights) weights[b * K + k] = wk;
+            sr += mul_rn(wk, v.x);
+            sg += mul_rn(wk, v.y);
+            sb += mul_rn(wk, v.z);
+            sd += mul_rn(wk, zk);
             sw += wk;
-        }
-    };
-    if constexpr (NCH > 0) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) step(c, c);
-    } else {
-        for (int c = 0; c < (K + 63) / 64; ++c) {
-            load(0, 64 * c + lane);
-            step(c, 0);
         }
     }
     sr = wave_sum(sr);
@@ -246,8 +302,8 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
     if (n_rays == 0) return PNR_OK;
     const int64_t blocks = (n_rays + 3) / 4;
     const int nch = (K + 63) / 64;
-    auto kern = nch == 1 ? k_composite<1> : nch == 2 ? k_composite<2> : nch == 3 ? k_composite<3>
-              : nch == 4 ? k_composite<4> : k_composite<0>;
+    auto kern = nch == 1 ? k_composite_s<1> : nch == 2 ? k_composite_s<2> : nch == 3 ? k_composite_s<3>
+              : nch == 4 ? k_composite_s<4> : k_composite;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, z, raw, rays,
                        n_rays, K, white_bkgd, weights, rgb, depth);
     return launch_ok("composite") ? PNR_OK : PNR_ERR_HIP;

@@ -50,6 +50,42 @@ __device__ __forceinline__ T wave_sum(T v) {
     return v;
 }
 
+// ---- DPP wave64 scans / reductions (GFX9 row_shr, row_bcast:15/31, wave_shr:1; no LDS) ----
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_f(float old, float src) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(src), CTRL,
+                                                      ROW_MASK, 0xf, false));
+}
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ double dpp_d(double old, double src) {
+    const long long o = __double_as_longlong(old), v = __double_as_longlong(src);
+    const int lo = __builtin_amdgcn_update_dpp((int)o, (int)v, CTRL, ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(v >> 32), CTRL, ROW_MASK, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// inclusive product scan over the 64 lanes (lanes out of range contribute 1)
+__device__ __forceinline__ double wave_scan_mul(double x) {
+    x *= dpp_d<0x111>(1.0, x);          // row_shr:1
+    x *= dpp_d<0x112>(1.0, x);          // row_shr:2
+    x *= dpp_d<0x114>(1.0, x);          // row_shr:4
+    x *= dpp_d<0x118>(1.0, x);          // row_shr:8
+    x *= dpp_d<0x142, 0xa>(1.0, x);     // row_bcast:15 -> rows 1, 3
+    x *= dpp_d<0x143, 0xc>(1.0, x);     // row_bcast:31 -> rows 2, 3
+    return x;
+}
+// value of lane - 1 (lane 0: `first`)
+__device__ __forceinline__ double wave_shr1(double x, double first) { return dpp_d<0x138>(first, x); }
+// sum over the 64 lanes, returned wave-uniform
+__device__ __forceinline__ float wave_sum_dpp(float x) {
+    x += dpp_f<0x111>(0.f, x);
+    x += dpp_f<0x112>(0.f, x);
+    x += dpp_f<0x114>(0.f, x);
+    x += dpp_f<0x118>(0.f, x);
+    x += dpp_f<0x142, 0xa>(0.f, x);
+    x += dpp_f<0x143, 0xc>(0.f, x);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
