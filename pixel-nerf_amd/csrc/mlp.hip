@@ -513,6 +513,12 @@ __device__ __forceinline__ void split_f16x4(const f4 &v, float s, u2 &p0, u2 &p1
 // B-fragment ds_read_b128 of every lane group hit 16 distinct 16-B bank quads.
 constexpr int ROWH = H + 16;                    // halves per column row
 constexpr int PART_HALVES = COLS * ROWH;        // one part (67,584 B)
+// Swizzle: the 16-B chunk index of element k (k >> 3) is XORed with (column >> 2) & 3.
+// With the 1056-B pitch the B reads stay conflict-free and the producers' 8-B stores
+// (16 columns x one chunk) drop from 4-way to 2-way bank conflicts.  k % 4 == 0.
+__device__ __forceinline__ int swz(int col, int k) {
+    return 8 * ((k >> 3) ^ ((col >> 2) & 3)) + (k & 7);
+}
 
 // acc[r][c] += (W 2^eW)(IN 2^e) over NKS k-steps of 32 from the pre-split LDS image:
 // no staging, no split, no barrier inside the layer (waves run free).  A fragments
@@ -609,7 +615,7 @@ __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
             const f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
-            put_split4(P0, P1, col * ROWH + 16 * (RTW * wave + r) + 4 * g, o, sc);
+            put_split4(P0, P1, col * ROWH + swz(col, 16 * (RTW * wave + r) + 4 * g), o, sc);
         }
     }
 }
@@ -753,8 +759,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     float *cmax = gtab + COLS * 8;           // PREC 3: per-column partial maxima (64 x 8)
     int *ecol = reinterpret_cast<int *>(cmax + COLS * 8);
     gc.hdr = a.packed;
-    gc.pb0 = P0 + cl * ROWH + 8 * g;
-    gc.pb1 = P1 + cl * ROWH + 8 * g;
+    // B fragment (column 16c + cl, k 32 ks + 8g): swz keeps it linear in ks and c
+    gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
+    gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
     gc.wave = wave;
     gc.lane = lane;
@@ -846,7 +853,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     const float sc = __builtin_ldexpf(1.f, e);
 #pragma unroll
                     for (int i = 0; i < FPT / 4; ++i)
-                        put_split4(P0, P1, col * ROWH + FPT * qt + 4 * i,
+                        put_split4(P0, P1, col * ROWH + swz(col, FPT * qt + 4 * i),
                                    f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]}, sc);
                     if (qt == 0) ecol[col] = e;
                 } else {
@@ -936,8 +943,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                         m = wave_max(m);
                         const int e = scale_exp(m);
                         const float sc = __builtin_ldexpf(1.f, e);
-                        put_split4(P0, P1, cj * ROWH + lane * 4, zh[0], sc);
-                        put_split4(P0, P1, cj * ROWH + 256 + lane * 4, zh[1], sc);
+                        put_split4(P0, P1, cj * ROWH + swz(cj, lane * 4), zh[0], sc);
+                        put_split4(P0, P1, cj * ROWH + swz(cj, 256 + lane * 4), zh[1], sc);
                         if (lane == 0) ecol[cj] = e;
                     }
                 }
