@@ -525,22 +525,33 @@ __device__ __forceinline__ int swz(int col, int k) {
 // stream from L2 A_DIST row tiles ahead; the last k-step is peeled so no load is in
 // flight when the accumulators are handed back.
 //   pb0 / pb1: P0 / P1 at (column cl, k 8g) of column tile 0
+#ifndef PNR_H_DIST
+#define PNR_H_DIST 3
+#endif
+constexpr int H_DIST = PNR_H_DIST;               // f16 weight prefetch distance (row tiles)
+constexpr int H_RING = H_DIST < RTW ? RTW : 2 * RTW;   // register ring slots
+static_assert(H_DIST < H_RING && H_RING % RTW == 0, "ring");
 template <int NKS>
 __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
                                          const _Float16 *pb1) {
-    h8 ra[A_RING][2];
-    auto loadA = [&](h8 (&dst)[2], int ks, int r) {
+    constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
+    static_assert(NKS % U == 0, "k-steps");
+    h8 ra[H_RING][2];
+    // row tile t = RTW * ks + r of the layer's stream lives in slot t % H_RING
+    auto loadA = [&](int slot, int ks, int r) {
 #ifdef PNR_ABLATE_WSTREAM
         ks = 0;  // diagnostic: no weight stream
 #endif
         const float *src = wp + (int64_t)ks * SKS16_FLOATS + r * SRT16_FLOATS;
-        dst[0] = *reinterpret_cast<const h8 *>(src);
-        dst[1] = *reinterpret_cast<const h8 *>(src + 256);
+        ra[slot][0] = *reinterpret_cast<const h8 *>(src);
+        ra[slot][1] = *reinterpret_cast<const h8 *>(src + 256);
     };
 #pragma unroll
-    for (int r = 0; r < A_DIST; ++r) loadA(ra[r], 0, r);
-    auto kstep = [&](int ks, auto last_tag) {
-        constexpr bool last = decltype(last_tag)::value;
+    for (int t = 0; t < H_DIST; ++t) loadA(t, t / RTW, t % RTW);
+    // one k-step; ph = ks % U (static), tail = this is one of the last U k-steps
+    auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
+        constexpr int ph = decltype(ph_tag)::value;
+        constexpr bool tail = decltype(tail_tag)::value;
         h8 b0[CT], b1[CT];
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
@@ -549,11 +560,10 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
         }
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
-            const int rn = r + A_DIST;
-            if (rn < RTW) loadA(ra[rn % A_RING], ks, rn);
-            else if (!last) loadA(ra[rn % A_RING], ks + 1, rn - RTW);
+            const int tn = ph * RTW + r + H_DIST;          // prefetch target, relative to the iteration
+            if (!tail || tn < U * RTW) loadA(tn % H_RING, ks - ph + tn / RTW, tn % RTW);
             __builtin_amdgcn_sched_barrier(0);
-            const h8 *a = ra[r % A_RING];
+            const h8 *a = ra[(ph * RTW + r) % H_RING];
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
                 f4 v = acc[r][c];
@@ -564,9 +574,13 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
             }
         }
     };
+    auto iter = [&](int ks0, auto tail_tag) {
+        kstep(ks0, std::integral_constant<int, 0>{}, tail_tag);
+        if constexpr (U > 1) kstep(ks0 + 1, std::integral_constant<int, 1>{}, tail_tag);
+    };
 #pragma unroll 1
-    for (int ks = 0; ks + 1 < NKS; ++ks) kstep(ks, std::false_type{});
-    kstep(NKS - 1, std::true_type{});
+    for (int ks = 0; ks + U < NKS; ks += U) iter(ks, std::false_type{});
+    iter(NKS - U, std::true_type{});
 }
 
 // 4 (or 8) fp32 values -> scaled fp16 parts written to P0 / P1 at half offset `off`
@@ -775,6 +789,17 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 
     // relu(acc) -> the next GEMM's input image (callers barrier before and after)
     auto publish_relu = [&](const Acc &acc) {
+#ifdef PNR_GEMM_ONLY
+        {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
+            float t = 0.f;
+#pragma unroll
+            for (int r = 0; r < RTW; ++r)
+#pragma unroll
+                for (int c = 0; c < CT; ++c) t += acc[r][c].x + acc[r][c].y + acc[r][c].z + acc[r][c].w;
+            cmax[tid & 511] = t;
+            return;
+        }
+#endif
         if constexpr (PREC == 3) {
             relu_colmax(acc, cmax, wave, lane);
             __syncthreads();
@@ -784,6 +809,12 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
     };
 
+#ifdef PNR_GEMM_ONLY
+    if (tid < COLS) ecol[tid] = -8;
+    for (int i = tid; i < 2 * PART_HALVES; i += NTHR)   // nonzero operands (power / clock)
+        P0[i] = (_Float16)(0.25f + 0.001f * (float)(i % 977));
+    __syncthreads();
+#endif
     Acc x, h;
     for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         const int64_t p_raw = tile * COLS + col;
@@ -908,6 +939,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 // z = bilinear latent gather (torch's nw, ne, sw, se summation order).
                 // Wave w walks its COLS / WAVES columns; each load instruction reads one
                 // contiguous 1 KB half of a corner's 2 KB channel row (lane = 4 channels).
+#ifdef PNR_GEMM_ONLY
+                if (0)
+#endif
 #pragma unroll 4
                 for (int j = 0; j < COLS / WAVES; ++j) {
                     const int cj = (COLS / WAVES) * wave + j;
@@ -1014,6 +1048,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         publish_relu(x);
         __syncthreads();
         PT(gc, 3);
+#ifdef PNR_GEMM_ONLY
+        if (0)
+#endif
         if (PREC == 3 && wave < CT) {
             // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col
             const float *wo = a.packed + L.off_lin_out + lane * 4;
