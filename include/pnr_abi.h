@@ -201,6 +201,15 @@ int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n
                   int32_t k, int32_t white_bkgd, float *weights, float *rgb, float *depth,
                   pnr_stream_t stream);
 
+/* ---- ray generation ------------------------------------------------------------ */
+/* Replaces: util.gen_rays (util.py:238-276) with unproj_map (util.py:113-143), ndc=False.
+ * poses (n_images, pose_rows, 4) row-major camera-to-world (pose_rows 3 or 4); focal
+ * (fx, fy) and principal point (cx, cy) in pixels, as the reference's float(f[0]) etc.;
+ * rays (n_images, height, width, 8) = [o, d (unit), near, far]. */
+int pnr_gen_rays(const float *poses, int64_t n_images, int32_t pose_rows, int32_t width,
+                 int32_t height, float fx, float fy, float cx, float cy, float z_near,
+                 float z_far, float *rays, pnr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

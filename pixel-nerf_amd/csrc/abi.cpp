@@ -15,6 +15,8 @@ int launch_sample_coarse(const float *, int64_t, int, const float *, int, float 
 int launch_sample_fine(const float *, int64_t, int, const float *, const float *, const float *,
                        int, int, float, const float *, const float *, const float *, int, float *,
                        hipStream_t);
+int launch_gen_rays(const float *, int64_t, int, int, int, float, float, float, float, float, float,
+                    float *, hipStream_t);
 int launch_composite(const float *, const float *, const float *, int64_t, int, int, float *,
                      float *, float *, hipStream_t);
 size_t mlp_packed_bytes(const pnr_mlp_desc &);
@@ -259,6 +261,18 @@ int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n
     if (!z || !raw || !rays || !rgb || !depth) return fail(PNR_ERR_INVALID, "pnr_composite: NULL");
     if ((reinterpret_cast<uintptr_t>(raw) & 15) != 0) return fail(PNR_ERR_INVALID, "raw must be 16-byte aligned");
     return launch_composite(z, raw, rays, n_rays, k, white_bkgd, weights, rgb, depth, (hipStream_t)stream);
+}
+
+int pnr_gen_rays(const float *poses, int64_t n_images, int32_t pose_rows, int32_t width, int32_t height,
+                 float fx, float fy, float cx, float cy, float z_near, float z_far, float *rays,
+                 pnr_stream_t stream) {
+    if (n_images < 0 || width < 0 || height < 0) return fail(PNR_ERR_INVALID, "pnr_gen_rays: bad sizes");
+    if (pose_rows != 3 && pose_rows != 4) return fail(PNR_ERR_INVALID, "pnr_gen_rays: pose_rows must be 3 or 4");
+    if (n_images == 0 || width == 0 || height == 0) return PNR_OK;
+    if (!poses || !rays) return fail(PNR_ERR_INVALID, "pnr_gen_rays: NULL");
+    if ((reinterpret_cast<uintptr_t>(rays) & 15) != 0) return fail(PNR_ERR_INVALID, "rays must be 16-byte aligned");
+    return launch_gen_rays(poses, n_images, pose_rows, width, height, fx, fy, cx, cy, z_near, z_far, rays,
+                           (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -266,6 +266,38 @@ __global__ __launch_bounds__(256) void k_composite(
 }
 
 // ---------------------------------------------------------------------------
+// gen_rays — util.py:113-143 (unproj_map) + 238-276.  One thread per pixel:
+//   X = (x - cx) / fx, Y = (y - cy) / fy, u = (X, -Y, -1) / |(X, -Y, -1)|,
+//   ray = [t_wc, R_wc u, near, far]   (pose row-major, rows 3 or 4 per image)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gen_rays(const float *__restrict__ poses, int pose_rows,
+                                                  int64_t n_pix, int width, int height, float fx,
+                                                  float fy, float cx, float cy, float near,
+                                                  float far, float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_pix) return;
+    const int64_t hw = (int64_t)width * height;
+    const int64_t img = i / hw;
+    const int pix = (int)(i - img * hw);
+    const int y = pix / width, x = pix - y * width;
+    const float X = __fdiv_rn(sub_rn((float)x, cx), fx);
+    const float Y = __fdiv_rn(sub_rn((float)y, cy), fy);
+    const float nrm = __fsqrt_rn(add_rn(add_rn(mul_rn(X, X), mul_rn(Y, Y)), 1.0f));
+    const float u0 = __fdiv_rn(X, nrm), u1 = __fdiv_rn(-Y, nrm), u2 = __fdiv_rn(-1.0f, nrm);
+    const float *P = poses + img * pose_rows * 4;
+    f4 a, b;
+    float d[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+        d[r] = add_rn(add_rn(mul_rn(P[4 * r], u0), mul_rn(P[4 * r + 1], u1)), mul_rn(P[4 * r + 2], u2));
+    a = f4{P[3], P[7], P[11], d[0]};
+    b = f4{d[1], d[2], near, far};
+    f4 *o = reinterpret_cast<f4 *>(out + i * 8);
+    o[0] = a;
+    o[1] = b;
+}
+
+// ---------------------------------------------------------------------------
 // host launchers (validated by the extern "C" layer in abi.cpp)
 // ---------------------------------------------------------------------------
 int launch_sample_coarse(const float *rays, int64_t n_rays, int kc, const float *u, int lindisp,
@@ -307,6 +339,16 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, z, raw, rays,
                        n_rays, K, white_bkgd, weights, rgb, depth);
     return launch_ok("composite") ? PNR_OK : PNR_ERR_HIP;
+}
+
+int launch_gen_rays(const float *poses, int64_t n_images, int pose_rows, int width, int height,
+                    float fx, float fy, float cx, float cy, float near, float far, float *rays,
+                    hipStream_t st) {
+    const int64_t n = n_images * width * height;
+    if (n == 0) return PNR_OK;
+    hipLaunchKernelGGL(k_gen_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, poses, pose_rows,
+                       n, width, height, fx, fy, cx, cy, near, far, rays);
+    return launch_ok("gen_rays") ? PNR_OK : PNR_ERR_HIP;
 }
 
 }  // namespace pnr

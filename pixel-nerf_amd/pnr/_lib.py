@@ -83,6 +83,7 @@ SIGNATURES = {
     "pnr_sample_fine": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f, c_vp,
                                 c_vp, c_vp, c_i32, c_vp, c_vp]),
     "pnr_composite": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "pnr_gen_rays": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_f, c_f, c_f, c_f, c_f, c_f, c_vp, c_vp]),
 }
 
 _lib = None

@@ -75,8 +75,38 @@ def unproj_map(width, height, f, c=None, device="cpu"):
     return d
 
 
+def _focal_c(width, height, focal, c):
+    """(fx, fy, cx, cy) as the reference resolves them (util.py:124-134, 250-251)."""
+    f = focal.squeeze() if torch.is_tensor(focal) else focal
+    if isinstance(f, (float, int)):
+        fx = fy = float(f)
+    else:
+        f = torch.as_tensor(f).reshape(-1)
+        fx, fy = float(f[0]), float(f[-1])
+    if c is None:
+        cx, cy = width * 0.5, height * 0.5
+    else:
+        c = torch.as_tensor(c).reshape(-1)
+        cx, cy = float(c[0]), float(c[-1] if c.numel() > 1 else c[0])
+    return fx, fy, cx, cy
+
+
 def gen_rays(poses, width, height, focal, z_near, z_far, c=None):
-    """Camera rays for every pixel of every pose: (NV, H, W, 8) (util.py:238-276)."""
+    """Camera rays for every pixel of every pose: (NV, H, W, 8) (util.py:238-276).
+
+    Poses on the HIP device run the ``pnr_gen_rays`` kernel (the rays are born in HBM);
+    host poses use the host restatement below, as the reference's host code does."""
+    if poses.is_cuda:
+        from . import _lib
+
+        fx, fy, cx, cy = _focal_c(width, height, focal, c)
+        p = poses.detach().to(torch.float32).contiguous()
+        rows = p.shape[-2]
+        out = torch.empty(p.shape[0], height, width, 8, dtype=torch.float32, device=p.device)
+        _lib.check(_lib.load().pnr_gen_rays(_lib.ptr(p), p.shape[0], rows, width, height, fx, fy, cx,
+                                            cy, float(z_near), float(z_far), _lib.ptr(out),
+                                            _lib.stream_of(p.device)), "pnr_gen_rays")
+        return out
     nv = poses.shape[0]
     device = poses.device
     f = focal.squeeze() if torch.is_tensor(focal) else focal

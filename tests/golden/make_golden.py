@@ -305,6 +305,23 @@ def composite_case(name, seed=5, B=48, K=24, white_bkgd=True):
                      rgb=rgb.numpy(), depth=depth.numpy())
 
 
+def gen_rays_case(name):
+    """util.gen_rays (util.py:238-276): (fx, fy) + principal point, and scalar focal with
+    the default image-centre principal point."""
+    import util
+
+    poses = synth.srn_poses([0.0, 37.0, 141.0], radius=1.7)
+    focal = torch.tensor([52.0, 55.0])
+    c = torch.tensor([19.5, 16.0])
+    with torch.no_grad():
+        r1 = util.gen_rays(poses, 40, 30, focal, 0.8, 1.8, c=c)
+        r2 = util.gen_rays(poses[:2], 33, 21, torch.tensor(61.25), 0.01, 4.0)
+    cfg = dict(name=name, w1=40, h1=30, near1=0.8, far1=1.8, w2=33, h2=21, near2=0.01, far2=4.0,
+               focal2=61.25)
+    return cfg, dict(poses=poses.numpy(), focal1=focal.numpy(), c1=c.numpy(), rays1=r1.numpy(),
+                     rays2=r2.numpy())
+
+
 def save(cfg, arrays):
     path = os.path.join(HERE, cfg["name"] + ".npz")
     np.savez_compressed(path, config=np.array(json.dumps(cfg)), **arrays)
@@ -373,6 +390,8 @@ def main():
                           n_coarse=64, n_fine=64, n_fine_depth=0, white_bkgd=False,
                           rng_seed=5, multi_obj_poses=sc["poses"][None],
                           focal_override=sc["focal"][None], c_override=sc["c"][None]))
+    if want("gen_rays"):
+        save(*gen_rays_case("gen_rays"))
     if want("fw_pointquery"):
         sc = synth.scene_srn(seed=0, n_rays=1)
         save(*point_query_case("fw_pointquery", seed=1, scene=sc, n_points=512))

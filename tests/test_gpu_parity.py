@@ -229,6 +229,27 @@ def test_point_query_dynamic_range(precision, lat_scale, w_scale):
                  atol=ATOL * max(1.0, mag))
 
 
+# ------------------------------------------------------------------- rays --
+def test_gen_rays_matches_reference_fixture():
+    """pnr_gen_rays (util.gen_rays on device poses) vs the reference's util.gen_rays
+    (tests/golden/gen_rays.npz): fx/fy + principal point, and scalar focal with the default
+    image-centre principal point; 3x4 poses too."""
+    from pnr import util
+
+    cfg, arr = fixtures.load("gen_rays")
+    poses = arr["poses"].to(DEV)
+    r1 = util.gen_rays(poses, cfg["w1"], cfg["h1"], arr["focal1"].to(DEV), cfg["near1"], cfg["far1"],
+                       c=arr["c1"].to(DEV))
+    r2 = util.gen_rays(poses[:2], cfg["w2"], cfg["h2"], torch.tensor(cfg["focal2"]), cfg["near2"],
+                       cfg["far2"])
+    r3 = util.gen_rays(poses[:, :3].contiguous(), cfg["w1"], cfg["h1"], arr["focal1"], cfg["near1"],
+                       cfg["far1"], c=arr["c1"])
+    assert r1.is_cuda and r2.is_cuda
+    assert_close(r1, arr["rays1"], "gen_rays focal (2,) + c", atol=2e-6, rtol=0)
+    assert_close(r2, arr["rays2"], "gen_rays scalar focal", atol=2e-6, rtol=0)
+    assert_close(r3, arr["rays1"], "gen_rays 3x4 poses", atol=2e-6, rtol=0)
+
+
 # ------------------------------------------------------------------ render --
 def compare_render(name, out, cfg, arr):
     c = out.coarse

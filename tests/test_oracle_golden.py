@@ -91,3 +91,18 @@ def test_oracle_point_query():
         of = ref_cpu.pixelnerf_forward(sd, scene, arr["xyz"], False, vd)
     torch.testing.assert_close(oc, arr["out_coarse"], atol=ATOL, rtol=0)
     torch.testing.assert_close(of, arr["out_fine"], atol=ATOL, rtol=0)
+
+
+def test_host_gen_rays_matches_reference():
+    """pnr.util.gen_rays on host tensors (the reference's host utility, restated) vs the
+    reference's util.gen_rays output (tests/golden/gen_rays.npz)."""
+    from pnr import util
+
+    cfg, arr = fixtures.load("gen_rays")
+    r1 = util.gen_rays(arr["poses"], cfg["w1"], cfg["h1"], arr["focal1"], cfg["near1"], cfg["far1"],
+                       c=arr["c1"])
+    r2 = util.gen_rays(arr["poses"][:2], cfg["w2"], cfg["h2"], torch.tensor(cfg["focal2"]),
+                       cfg["near2"], cfg["far2"])
+    assert r1.shape == arr["rays1"].shape and r2.shape == arr["rays2"].shape
+    assert (r1 - arr["rays1"]).abs().max() <= 1e-6
+    assert (r2 - arr["rays2"]).abs().max() <= 1e-6
