@@ -210,6 +210,36 @@ int pnr_gen_rays(const float *poses, int64_t n_images, int32_t pose_rows, int32_
                  int32_t height, float fx, float fy, float cx, float cy, float z_near,
                  float z_far, float *rays, pnr_stream_t stream);
 
+/* ---- training (autograd over the ray march) ------------ */
+/* Floats of the activation save of pnr_render_points for n_points points:
+ * per point features (64) | z (512) | relu(x) into fc_0 of each block (512 each) |
+ * relu(h) of each block (512 each) | relu(x) into lin_out (512), each region [point][width]. */
+size_t pnr_point_save_floats(const pnr_mlp_desc *desc, int64_t n_points);
+
+/* Replaces: the model call of NeRFRenderer.composite (nerf.py:182-216) under autograd:
+ * PixelNeRFNet.forward at the points o + z d of every ray (z (n_rays, k)), writing
+ * out (n_rays * k, 4) and, when `save` is not NULL, the activations the backward needs
+ * (n_views must be 1).  Workspace as pnr_point_query. */
+int pnr_render_points(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                      const pnr_rays *rays, const float *z, int32_t k, float *out, float *save,
+                      void *workspace, size_t workspace_bytes, pnr_stream_t stream);
+
+/* Replaces: autograd of NeRFRenderer.composite (nerf.py:225-247).  Given d_rgb (n_rays, 3),
+ * d_depth (n_rays, may be NULL) and d_weights (n_rays, k, may be NULL): d_raw (n_rays, k, 4)
+ * = d [rgb, sigma] and d_z (n_rays, k, may be NULL).  k <= 256. */
+int pnr_composite_backward(const float *z, const float *raw, const float *rays, int64_t n_rays,
+                           int32_t k, int32_t white_bkgd, const float *d_rgb, const float *d_depth,
+                           const float *d_weights, float *d_raw, float *d_z, pnr_stream_t stream);
+
+/* Replaces: autograd of the input stage of PixelNeRFNet.forward (models.py:156-221,
+ * code.py:30-42, encoder.py:80-109) for n_views == 1.  d_feat (n_rays * k, 64): gradient of
+ * the lin_in input; d_zlat (n_rays * k, 512): gradient of the sampled latent feature.
+ * Accumulates d_latent (channels-last, like scene->latent; may be NULL) and writes d_z
+ * (n_rays * k, may be NULL) = dL / d z_sample.  `packed` supplies the PE buffers. */
+int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                              const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
+                              const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,9 +23,15 @@ size_t mlp_packed_bytes(const pnr_mlp_desc &);
 int mlp_check_desc(const pnr_mlp_desc &);
 int mlp_pack(const pnr_mlp_weights &, void *, size_t, hipStream_t);
 size_t mlp_xsum_bytes(int ns);
+int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points);
+int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
+                         const float *, const float *, float *, float *, hipStream_t);
+int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, const float *, const float *,
+                         int, int, float, float, const float *, int, const float *, const float *, float *,
+                         float *, hipStream_t);
 int launch_point_mlp(const pnr_scene &, const pnr_mlp_desc &, const void *, const float *,
                      const float *, int, int64_t, const float *, const float *, int64_t, int64_t,
-                     float *, float *, hipStream_t);
+                     float *, float *, hipStream_t, float *save = nullptr);
 
 static thread_local char g_err[1024];
 
@@ -124,6 +130,67 @@ int pnr_point_query(const pnr_scene *scene, const pnr_mlp_desc *desc, const void
     return launch_point_mlp(*scene, *desc, packed, nullptr, nullptr, 0, 1, xyz, viewdirs,
                             points_per_obj, n_points, out, static_cast<float *>(workspace),
                             (hipStream_t)stream);
+}
+
+size_t pnr_point_save_floats(const pnr_mlp_desc *desc, int64_t n_points) {
+    if (!desc || n_points < 0 || mlp_check_desc(*desc) != PNR_OK) return 0;
+    return (size_t)mlp_save_floats(*desc, n_points);
+}
+
+static int check_rays_z(const pnr_scene *scene, const pnr_rays *rays, const float *z, int32_t k) {
+    if (!rays || (rays->n_rays > 0 && (!rays->rays || !z))) return fail(PNR_ERR_INVALID, "rays / z NULL");
+    if (rays->n_rays < 0 || k < 1) return fail(PNR_ERR_INVALID, "bad n_rays / k");
+    if (rays->rays_per_obj < 1 || rays->n_rays != rays->rays_per_obj * scene->n_obj)
+        return fail(PNR_ERR_INVALID, "n_rays must equal rays_per_obj * n_obj");
+    return PNR_OK;
+}
+
+int pnr_render_points(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                      const pnr_rays *rays, const float *z, int32_t k, float *out, float *save,
+                      void *workspace, size_t workspace_bytes, pnr_stream_t stream) {
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    if ((rc = check_desc_for_scene(desc, scene))) return rc;
+    if ((rc = check_rays_z(scene, rays, z, k))) return rc;
+    if (!packed || !out) return fail(PNR_ERR_INVALID, "pnr_render_points: NULL pointer");
+    if (save && scene->n_views != 1)
+        return fail(PNR_ERR_UNSUPPORTED, "activation save (training) implements n_views == 1");
+    const int64_t n_points = rays->n_rays * k;
+    if (n_points == 0) return PNR_OK;
+    const size_t need = pnr_point_query_workspace_bytes(scene, n_points);
+    if (need && (!workspace || workspace_bytes < need))
+        return fail(PNR_ERR_WORKSPACE, "pnr_render_points: workspace %zu < %zu", workspace_bytes, need);
+    return launch_point_mlp(*scene, *desc, packed, rays->rays, z, k, rays->rays_per_obj, nullptr, nullptr, 1,
+                            n_points, out, static_cast<float *>(workspace), (hipStream_t)stream, save);
+}
+
+int pnr_composite_backward(const float *z, const float *raw, const float *rays, int64_t n_rays, int32_t k,
+                           int32_t white_bkgd, const float *d_rgb, const float *d_depth,
+                           const float *d_weights, float *d_raw, float *d_z, pnr_stream_t stream) {
+    if (n_rays < 0 || k < 1) return fail(PNR_ERR_INVALID, "pnr_composite_backward: bad sizes");
+    if (k > 256) return fail(PNR_ERR_UNSUPPORTED, "pnr_composite_backward: k <= 256");
+    if (n_rays == 0) return PNR_OK;
+    if (!z || !raw || !rays || !d_rgb || !d_raw) return fail(PNR_ERR_INVALID, "pnr_composite_backward: NULL");
+    if (((reinterpret_cast<uintptr_t>(raw) | reinterpret_cast<uintptr_t>(d_raw)) & 15) != 0)
+        return fail(PNR_ERR_INVALID, "raw / d_raw must be 16-byte aligned");
+    return launch_composite_bwd(z, raw, rays, n_rays, k, white_bkgd, d_rgb, d_depth, d_weights, d_raw, d_z,
+                                (hipStream_t)stream);
+}
+
+int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                              const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
+                              const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream) {
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    if ((rc = check_desc_for_scene(desc, scene))) return rc;
+    if ((rc = check_rays_z(scene, rays, z, k))) return rc;
+    if (scene->n_views != 1) return fail(PNR_ERR_UNSUPPORTED, "input backward implements n_views == 1");
+    if (scene->latent_c != 512) return fail(PNR_ERR_UNSUPPORTED, "input backward: latent_c == 512");
+    if (!packed || !d_feat || !d_zlat) return fail(PNR_ERR_INVALID, "pnr_points_input_backward: NULL");
+    return launch_points_in_bwd(rays->rays, z, k, rays->rays_per_obj, rays->n_rays * k, scene->cams,
+                                scene->latent, scene->latent_h, scene->latent_w, scene->image_w,
+                                scene->image_h, static_cast<const float *>(packed), desc->pe_n, d_feat,
+                                d_zlat, d_latent, d_z, (hipStream_t)stream);
 }
 
 // workspace layout of pnr_render_forward

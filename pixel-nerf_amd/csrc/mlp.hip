@@ -275,13 +275,40 @@ struct Args {
     float *out;
     float *xsum;       // scratch: gridDim.x x 2 x (COLS * H) floats (x park, multi-view sum)
     int64_t n_tiles;
+    // training forward (NS == 1): activations for the backward, fp32 row-major [point][width]:
+    //   features (64) | z (512) | relu(x) into fc_0 of block b (512 each) |
+    //   relu(h) of block b (512 each) | relu(x) into lin_out (512)          (save_floats())
+    float *save;
 };
+
+// floats of the activation save per point (Args::save)
+__host__ __device__ constexpr int64_t save_floats_per_point(int n_blocks) {
+    return 64 + (int64_t)H * (2 + 2 * n_blocks);
+}
+
 
 __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
 typedef f4 Acc[RTW][CT];
+
+// relu(acc) of this wave's rows -> save slot [point][512] (points of this tile < n_points)
+__device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
+                                          int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int64_t p = tile * COLS + 16 * c + cl;
+        if (p >= n_points) continue;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            const f4 v = acc[r][c];
+            *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) =
+                f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        }
+    }
+}
 
 // acc[r][c] (+)= W(rows of this wave) * IN^T over nkb k-blocks.
 //   wp  : this layer's packed weights, already offset to this wave's first row
@@ -788,7 +815,12 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     const int col = tid / WAVES, qt = tid % WAVES;
 
     // relu(acc) -> the next GEMM's input image (callers barrier before and after)
-    auto publish_relu = [&](const Acc &acc) {
+    // activation save slots (training forward)
+    const int64_t P = a.n_points;
+    float *sv_f = a.save, *sv_z = a.save ? a.save + P * 64 : nullptr;
+    auto sv_slot = [&](int i) { return sv_z + P * H * (1 + i); };   // i: block b -> x_in, nb + b -> h, 2nb -> x_f
+    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx) {
+        if (a.save) save_relu(acc, sv_slot(save_idx), tile, P, wave, lane);
 #ifdef PNR_GEMM_ONLY
         {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
             float t = 0.f;
@@ -872,6 +904,12 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                         val = d == 0 ? vd[0] : (d == 1 ? vd[1] : vd[2]);
                     }
                     fv[i] = val;
+                }
+                if (a.save && p_raw < a.n_points) {
+#pragma unroll
+                    for (int i = 0; i < FPT / 4; ++i)
+                        *reinterpret_cast<f4 *>(sv_f + p_raw * 64 + FPT * qt + 4 * i) =
+                            f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
                 }
                 if constexpr (PREC == 3) {
                     // column max over its WAVES feature threads (adjacent lanes), scale, split
@@ -966,6 +1004,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                                   mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
                         if constexpr (PREC == 3) zh[half] = zz;
                         else *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
+                        if (a.save && blk == 0 && tile * COLS + cj < P)
+                            *reinterpret_cast<f4 *>(sv_z + (tile * COLS + cj) * H + ch) = zz;
                     }
                     if constexpr (PREC == 3) {
                         // column max over the wave (all 512 channels), scale, split
@@ -987,13 +1027,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 __syncthreads();
-                publish_relu(x);
+                publish_relu(x, tile, blk);
                 if constexpr (PREC != 0 && kParkX) park(x, xp);
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, g, false);
                 layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
                 __syncthreads();
-                publish_relu(h);
+                publish_relu(h, tile, L.n_blocks + blk);
                 __syncthreads();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp);
                 add_bias(x, bias + (3 + lz) * H, wave, g, true);
@@ -1031,13 +1071,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             __syncthreads();
-            publish_relu(x);
+            publish_relu(x, tile, blk);
             if constexpr (PREC != 0 && kParkX) park(x, xp);
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, g, false);
             layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
             __syncthreads();
-            publish_relu(h);
+            publish_relu(h, tile, L.n_blocks + blk);
             __syncthreads();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp);
             add_bias(x, bias + (2 + l0) * H, wave, g, true);
@@ -1045,7 +1085,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         __syncthreads();
-        publish_relu(x);
+        publish_relu(x, tile, 2 * L.n_blocks);
         __syncthreads();
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY
@@ -1201,6 +1241,10 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
     return PNR_OK;
 }
 
+int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points) {
+    return mlpk::save_floats_per_point(d.n_blocks) * n_points;
+}
+
 size_t mlp_xsum_bytes(int ns) {
     (void)ns;  // x park + multi-view sum, one pair of 128 KB regions per resident workgroup
     return sizeof(float) * (size_t)device_cu_count() * 2 * mlpk::COLS * mlpk::H;
@@ -1210,7 +1254,7 @@ size_t mlp_xsum_bytes(int ns) {
 int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *packed,
                      const float *rays, const float *zs, int K, int64_t rays_per_obj,
                      const float *xyz, const float *dirs, int64_t points_per_obj,
-                     int64_t n_points, float *out, float *xsum_ws, hipStream_t st) {
+                     int64_t n_points, float *out, float *xsum_ws, hipStream_t st, float *save) {
     if (n_points == 0) return PNR_OK;
     mlpk::Args a = {};
     a.packed = static_cast<const float *>(packed);
@@ -1225,6 +1269,7 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.out = out;
     a.xsum = xsum_ws;
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
+    a.save = save;
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
     // PREC 3: split image P0 + P1, gather records, column maxima, exponents = 139,520 B

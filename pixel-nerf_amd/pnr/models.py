@@ -332,14 +332,20 @@ class PixelNeRFNet(nn.Module):
             return "multi-view input needs combine_layer < n_blocks"
         return None
 
+    def needs_grad(self):
+        """Does a forward now have to build the autograd graph (training)?"""
+        lat = self.encoder.latent_cl
+        return any(p.requires_grad for n, p in self.named_parameters() if not n.startswith("encoder.")) \
+            or (lat.requires_grad and not self.stop_encoder_grad)
+
     def _require_hip(self):
         r = self.hip_unsupported_reason()
         if r:
             raise NotImplementedError("pnr: " + r)
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+        if torch.is_grad_enabled() and self.needs_grad():
             raise NotImplementedError(
-                "pnr: the HIP ray march is forward-only (training backward is SURVEY §8(f) "
-                "rank 2); run under torch.no_grad() or freeze the parameters")
+                "pnr: point queries are forward-only; training runs through "
+                "NeRFRenderer.forward (pnr/train.py). Use torch.no_grad() for queries")
 
     def hip_scene(self):
         lat = self.encoder.latent_cl

@@ -145,8 +145,53 @@ class NeRFRenderer(torch.nn.Module):
         from .models import PixelNeRFNet
 
         if isinstance(model, PixelNeRFNet):
+            if torch.is_grad_enabled() and model.needs_grad():
+                return self._forward_train(model, rays, sb, streams, want_weights)
             return self._forward_fused(model, rays, sb, streams, want_weights)
         return self._forward_callback(model, rays, sb, streams, want_weights)
+
+    def _forward_train(self, net, rays, sb, streams, want_weights):
+        """The reference's autograd graph (nerf.py:251-303) over the HIP kernels
+        (pnr/train.py): coarse pass, importance samples from the detached coarse weights
+        (nerf.py:130), depth samples with their gradient (nerf.py:150-161), sort, fine pass."""
+        from .train import Composite, RenderPoints, mlp_params
+
+        r = net.hip_unsupported_reason()
+        if r:
+            raise NotImplementedError("pnr: " + r)
+        if net.num_views_per_obj != 1:
+            raise NotImplementedError("pnr: the training path implements one source view per object")
+        if rays.device.type != "cuda":
+            raise ValueError("pnr: rays must be on the HIP device")
+        if self.training and self.noise_std > 0.0:
+            raise NotImplementedError("noise_std > 0 in training mode is not implemented")
+        kc = self.n_coarse
+        kf = self.n_fine if self.using_fine else 0
+        kfd = self.n_fine_depth if self.using_fine else 0
+        u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
+        lat = net.encoder.latent_cl
+        if net.stop_encoder_grad:
+            lat = lat.detach()
+        p_c = mlp_params(net.mlp_coarse)
+        z_c = ops.sample_coarse(rays, kc, u_c, self.lindisp)
+        raw_c = RenderPoints.apply(net, True, rays, z_c, lat, *p_c)
+        w_c, rgb_c, d_c = Composite.apply(z_c, raw_c, rays, self.white_bkgd)
+        outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, d_c, sb, want_weights))
+        if kf > 0:
+            nf = kf - kfd
+            with torch.no_grad():
+                z_ci = (ops.sample_fine(rays, z_c, w_c.detach(), d_c.detach(), nf, 0, self.depth_std, u_f, u_j,
+                                        None, self.lindisp) if nf > 0 else z_c)
+            parts = [z_ci]
+            if kfd > 0:
+                z_d = d_c.unsqueeze(1).repeat((1, kfd)) + n_d * self.depth_std
+                parts.append(torch.max(torch.min(z_d, rays[:, -1:]), rays[:, -2:-1]))
+            z_f = torch.sort(torch.cat(parts, -1), -1)[0].contiguous()
+            p_f = mlp_params(net.mlp_fine) if net.mlp_fine is not None else p_c
+            raw_f = RenderPoints.apply(net, False, rays, z_f, lat, *p_f)
+            w_f, rgb_f, d_f = Composite.apply(z_f, raw_f, rays, self.white_bkgd)
+            outputs.fine = self._pack_out(w_f, rgb_f, d_f, sb, want_weights)
+        return outputs
 
     def _pack_out(self, w, rgb, depth, sb, want_weights):
         d = DotMap(rgb=rgb.reshape(sb, -1, 3), depth=depth.reshape(sb, -1))

@@ -1,0 +1,169 @@
+"""Training path: autograd over the HIP ray march (BASELINE cfg5).
+
+The reference trains by running torch autograd through ``NeRFRenderer.forward``
+(nerf.py:251-303) and ``PixelNeRFNet.forward`` (models.py:146-266); the training step is
+train.py:182-283.  Here the same graph is built from HIP kernels:
+
+* ``RenderPoints``: the model at the points ``o + z d`` of every ray.
+  * **Forward** (``pnr_render_points``): the fused kernel, which saves the activations
+    the backward needs: features, the sampled latent z, and relu(x) / relu(h) per block.
+  * **Backward:**
+    * the sigmoid / relu head;
+    * ResnetFC as per-layer plain GEMMs on the saved activations, on hipBLASLt through
+      ``torch.matmul`` in fp32;
+    * ``pnr_points_input_backward`` for the input stage: the bilinear scatter into the
+      channels-last latent (grid_sample backward), and dL/dz of every sample through the
+      PE and the projection.
+* ``Composite``: ``pnr_composite`` forward and ``pnr_composite_backward``.
+
+The renderer wires them as the reference's autograd graph does:
+* the importance samples use the detached coarse weights (nerf.py:130);
+* the depth samples keep their gradient to the coarse depth (nerf.py:150-161, 292);
+* the fine depths are sorted with ``torch.sort`` (nerf.py:295), so the gradient follows
+  the permutation.
+
+Only n_views == 1 is implemented (the SRN training configuration).
+"""
+import torch
+
+from . import _lib, ops
+
+__all__ = ["RenderPoints", "Composite", "mlp_backward", "mlp_params"]
+
+
+def mlp_params(mlp):
+    """The ResnetFC parameters in registration order (what autograd tracks)."""
+    return list(mlp.parameters())
+
+
+def _save_views(save, P, n_blocks, H=512):
+    """Slices of the pnr_render_points activation save (include/pnr_abi.h)."""
+    feat = save[: P * 64].view(P, 64)
+    base = P * 64
+    z = save[base: base + P * H].view(P, H)
+
+    def slot(i):
+        o = base + P * H * (1 + i)
+        return save[o: o + P * H].view(P, H)
+
+    return feat, z, slot
+
+
+def mlp_backward(mlp, save, d_o, P):
+    """ResnetFC backward (resnetfc.py:132-184, n_views == 1) given dL/d(pre-head output)
+    ``d_o`` (P, 4).  Returns ({param: grad}, d_feat (P, 64), d_zlat (P, 512) or None)."""
+    nb = mlp.n_blocks
+    lin_z = list(getattr(mlp, "lin_z", []))
+    feat, z, slot = _save_views(save, P, nb)
+    g = {}
+    xf = slot(2 * nb)
+    W = mlp.lin_out.weight.detach()
+    g[mlp.lin_out.weight] = d_o.t() @ xf
+    g[mlp.lin_out.bias] = d_o.sum(0)
+    dx = (d_o @ W) * (xf > 0)
+    dz = None
+    for b in reversed(range(nb)):
+        blk = mlp.blocks[b]
+        hb, xb = slot(nb + b), slot(b)
+        w1, w0 = blk.fc_1.weight.detach(), blk.fc_0.weight.detach()
+        g[blk.fc_1.weight] = dx.t() @ hb
+        g[blk.fc_1.bias] = dx.sum(0)
+        dh = (dx @ w1) * (hb > 0)
+        g[blk.fc_0.weight] = dh.t() @ xb
+        g[blk.fc_0.bias] = dh.sum(0)
+        dx = dx + (dh @ w0) * (xb > 0)
+        if b < len(lin_z):
+            lz = lin_z[b]
+            g[lz.weight] = dx.t() @ z
+            g[lz.bias] = dx.sum(0)
+            t = dx @ lz.weight.detach()
+            dz = t if dz is None else dz + t
+    d_in = mlp.lin_in.weight.shape[1]
+    g[mlp.lin_in.weight] = dx.t() @ feat[:, :d_in]
+    g[mlp.lin_in.bias] = dx.sum(0)
+    d_feat = torch.zeros(P, 64, device=dx.device, dtype=torch.float32)
+    d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
+    return g, d_feat, dz
+
+
+class RenderPoints(torch.autograd.Function):
+    """raw (B, K, 4) = PixelNeRFNet at o + z d (models.py:146-266, via nerf.py:182-216),
+    differentiable in z, the encoder latent (channels-last) and the MLP parameters."""
+
+    @staticmethod
+    def forward(ctx, net, coarse, rays, z, latent_cl, *params):
+        mlp = net.mlp_coarse if (coarse or net.mlp_fine is None) else net.mlp_fine
+        desc, packed = mlp.packed(net.code, net.mlp_precision)
+        sc = net.hip_scene()
+        B, K = z.shape
+        P = B * K
+        lib = _lib.load()
+        dev = z.device
+        n_save = lib.pnr_point_save_floats(desc, P)
+        if n_save == 0:
+            _lib.check(-1, "pnr_point_save_floats")
+        save = torch.empty(n_save, dtype=torch.float32, device=dev)
+        ws_bytes = lib.pnr_point_query_workspace_bytes(sc, P)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        out = torch.empty(P, 4, dtype=torch.float32, device=dev)
+        r = _lib.Rays(_lib.ptr(rays), B, B // net.num_objs)
+        _lib.check(lib.pnr_render_points(sc, desc, _lib.ptr(packed), r, _lib.ptr(z), K, _lib.ptr(out),
+                                         _lib.ptr(save), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev)),
+                   "pnr_render_points")
+        ctx.save_for_backward(rays, z, out, save, latent_cl)
+        ctx.net, ctx.mlp, ctx.desc, ctx.packed, ctx.params = net, mlp, desc, packed, params
+        return out.view(B, K, 4)
+
+    @staticmethod
+    def backward(ctx, d_out):
+        rays, z, out, save, latent_cl = ctx.saved_tensors
+        net, mlp = ctx.net, ctx.mlp
+        B, K = z.shape
+        P = B * K
+        d_out = d_out.reshape(P, 4).float()
+        # head: [sigmoid(rgb), relu(sigma)] (models.py:258-265)
+        d_o = torch.cat([d_out[:, :3] * out[:, :3] * (1.0 - out[:, :3]),
+                         d_out[:, 3:] * (out[:, 3:] > 0)], dim=1)
+        g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P)
+        need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        d_z = torch.empty(P, dtype=torch.float32, device=z.device) if need_z else None
+        d_lat = torch.zeros_like(latent_cl) if need_lat else None
+        if need_z or need_lat:
+            if d_zlat is None:
+                d_zlat = torch.zeros(P, 512, dtype=torch.float32, device=z.device)
+            lib = _lib.load()
+            r = _lib.Rays(_lib.ptr(rays), B, B // net.num_objs)
+            _lib.check(lib.pnr_points_input_backward(net.hip_scene(), ctx.desc, _lib.ptr(ctx.packed), r,
+                                                     _lib.ptr(z), K, _lib.ptr(d_feat.contiguous()),
+                                                     _lib.ptr(d_zlat.contiguous()), _lib.ptr(d_lat),
+                                                     _lib.ptr(d_z), _lib.stream_of(z.device)),
+                       "pnr_points_input_backward")
+        grads = [g.get(p) for p in ctx.params]
+        return (None, None, None, d_z.view(B, K) if need_z else None, d_lat, *grads)
+
+
+class Composite(torch.autograd.Function):
+    """(weights, rgb, depth) of NeRFRenderer.composite (nerf.py:225-247) with its backward."""
+
+    @staticmethod
+    def forward(ctx, z, raw, rays, white_bkgd):
+        w, rgb, depth = ops.composite(z, raw, rays, white_bkgd, want_weights=True)
+        ctx.save_for_backward(z, raw, rays)
+        ctx.white_bkgd = white_bkgd
+        return w, rgb, depth
+
+    @staticmethod
+    def backward(ctx, d_w, d_rgb, d_depth):
+        z, raw, rays = ctx.saved_tensors
+        B, K = z.shape
+        if d_rgb is None:
+            d_rgb = torch.zeros(B, 3, dtype=torch.float32, device=z.device)
+        d_raw = torch.empty(B, K, 4, dtype=torch.float32, device=z.device)
+        d_z = torch.empty(B, K, dtype=torch.float32, device=z.device) if ctx.needs_input_grad[0] else None
+        lib = _lib.load()
+        _lib.check(lib.pnr_composite_backward(
+            _lib.ptr(z), _lib.ptr(raw), _lib.ptr(rays), B, K, int(bool(ctx.white_bkgd)),
+            _lib.ptr(d_rgb.contiguous()), _lib.ptr(d_depth.contiguous() if d_depth is not None else None),
+            _lib.ptr(d_w.contiguous() if d_w is not None else None), _lib.ptr(d_raw), _lib.ptr(d_z),
+            _lib.stream_of(z.device)), "pnr_composite_backward")
+        return d_z, d_raw, None, None

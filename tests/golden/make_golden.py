@@ -305,6 +305,53 @@ def composite_case(name, seed=5, B=48, K=24, white_bkgd=True):
                      rgb=rgb.numpy(), depth=depth.numpy())
 
 
+def train_case(name, *, d_hidden=32, d_latent=64, seed=21, rng_seed=6, sb=2, rays_per_obj=12,
+               n_coarse=16, n_fine=12, n_fine_depth=4, white_bkgd=True):
+    """One training step's loss and gradients (train.py:182-283: MSE(coarse) + MSE(fine),
+    lambda = 1) through the reference renderer + model under autograd, with the depth
+    samples' gradient path (nerf.py:292, depth not detached).  The encoder latent is a
+    leaf (what SpatialEncoder.forward would hand the trunk's backward)."""
+    from render import NeRFRenderer
+
+    sc = synth.scene_multiview(seed=9, n_views=sb, n_rays=sb * rays_per_obj, channels=d_latent,
+                               h_l=6, w_l=7)
+    poses = sc["poses"].reshape(sb, 1, 4, 4)
+    focal = torch.tensor([[90.0, 95.0], [80.0, 85.0]])[:sb]
+    c = torch.tensor([[31.0, 30.0], [33.0, 29.0]])[:sb]
+    latent = sc["latent"].clone().requires_grad_(True)
+    net = build_reference_net(d_hidden, d_latent, seed, latent, poses, focal, c, sc["width"],
+                              sc["height"])
+    net.train()
+    for k, p in net.named_parameters():
+        p.requires_grad_(not k.startswith("encoder."))
+    # keep the latent leaf in the graph (fake_forward cloned it)
+    net.encoder.latent = latent
+    renderer = NeRFRenderer(n_coarse=n_coarse, n_fine=n_fine, n_fine_depth=n_fine_depth,
+                            depth_std=0.05, white_bkgd=white_bkgd, eval_batch_size=100000)
+    rays = sc["rays"].reshape(sb, rays_per_obj, 8)
+    B = sb * rays_per_obj
+    u_c, u_f, u_j, n_d = synth.rng_streams(rng_seed, B, n_coarse, n_fine, n_fine_depth)
+    target = torch.from_numpy(synth.hash_uniform(rng_seed + 100, B * 3).astype(np.float32)).reshape(sb, -1, 3)
+    with injected_rng(u_c, u_f, u_j, n_d):
+        out = renderer(net, rays, want_weights=True)
+    loss = torch.nn.functional.mse_loss(out.coarse.rgb, target) + \
+        torch.nn.functional.mse_loss(out.fine.rgb, target)
+    loss.backward()
+    cfg = dict(name=name, d_hidden=d_hidden, d_latent=d_latent, seed=seed, rng_seed=rng_seed, sb=sb,
+               n_coarse=n_coarse, n_fine=n_fine, n_fine_depth=n_fine_depth, depth_std=0.05,
+               white_bkgd=white_bkgd, width=sc["width"], height=sc["height"],
+               latent_seed=sc["latent_seed"])
+    arrays = dict(rays=rays.numpy(), poses=poses.numpy(), focal=focal.numpy(), c=c.numpy(),
+                  latent=latent.detach().numpy(), target=target.numpy(), u_coarse=u_c.numpy(),
+                  u_fine=u_f.numpy(), u_fine_jit=u_j.numpy(), n_depth=n_d.numpy(),
+                  loss=np.float32(loss.item()), coarse_rgb=out.coarse.rgb.detach().numpy(),
+                  fine_rgb=out.fine.rgb.detach().numpy(), grad_latent=latent.grad.numpy())
+    for k, p in net.named_parameters():
+        if p.grad is not None:
+            arrays["grad." + k] = p.grad.numpy()
+    return cfg, arrays
+
+
 def gen_rays_case(name):
     """util.gen_rays (util.py:238-276): (fx, fy) + principal point, and scalar focal with
     the default image-centre principal point."""
@@ -390,6 +437,8 @@ def main():
                           n_coarse=64, n_fine=64, n_fine_depth=0, white_bkgd=False,
                           rng_seed=5, multi_obj_poses=sc["poses"][None],
                           focal_override=sc["focal"][None], c_override=sc["c"][None]))
+    if want("train_step"):
+        save(*train_case("train_step"))
     if want("gen_rays"):
         save(*gen_rays_case("gen_rays"))
     if want("fw_pointquery"):

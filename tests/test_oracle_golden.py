@@ -106,3 +106,42 @@ def test_host_gen_rays_matches_reference():
     assert r1.shape == arr["rays1"].shape and r2.shape == arr["rays2"].shape
     assert (r1 - arr["rays1"]).abs().max() <= 1e-6
     assert (r2 - arr["rays2"]).abs().max() <= 1e-6
+
+
+def oracle_train_step(cfg, arr, sd, latent):
+    """Loss of one training step (train.py:254-283) through the oracle under autograd."""
+    scene = ref_cpu.Scene(latent, arr["poses"], arr["focal"], cfg["width"], cfg["height"], arr["c"])
+
+    def model_fn(pts, coarse, dirs):
+        return ref_cpu.pixelnerf_forward(sd, scene, pts, coarse, dirs, d_latent=cfg["d_latent"])
+
+    streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
+    out = ref_cpu.render(model_fn, arr["rays"], cfg["n_coarse"], cfg["n_fine"], cfg["n_fine_depth"],
+                         streams, cfg["white_bkgd"], depth_std=cfg["depth_std"])
+    mse = torch.nn.functional.mse_loss
+    return mse(out["coarse"]["rgb"], arr["target"]) + mse(out["fine"]["rgb"], arr["target"]), out
+
+
+def test_oracle_training_gradients_match_reference():
+    """Oracle autograd reproduces the reference's training-step loss and every MLP / latent
+    gradient (incl. the depth-sample path, nerf.py:292) of tests/golden/train_step.npz."""
+    from pnr import synth
+
+    torch.set_num_threads(4)
+    cfg, arr = fixtures.load("train_step")
+    sd = synth.pixelnerf_state(cfg["seed"], d_latent=cfg["d_latent"], d_hidden=cfg["d_hidden"])
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith("mlp_")}
+    sd.update(params)
+    latent = arr["latent"].clone().requires_grad_(True)
+    loss, out = oracle_train_step(cfg, arr, sd, latent)
+    loss.backward()
+    assert abs(loss.item() - float(arr["loss"])) <= 1e-6
+    torch.testing.assert_close(out["fine"]["rgb"], arr["fine_rgb"], atol=1e-6, rtol=0)
+    torch.testing.assert_close(latent.grad, arr["grad_latent"], atol=1e-6, rtol=1e-4)
+    n = 0
+    for k, p in params.items():
+        ref = arr.get("grad." + k)
+        assert ref is not None, k
+        torch.testing.assert_close(p.grad, ref, atol=1e-6, rtol=1e-4, msg=k)
+        n += 1
+    assert n == len([k for k in arr if k.startswith("grad.mlp_")])
