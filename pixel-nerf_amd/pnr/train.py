@@ -9,8 +9,8 @@ train.py:182-283.  Here the same graph is built from HIP kernels:
     the backward needs: features, the sampled latent z, and relu(x) / relu(h) per block.
   * **Backward:**
     * the sigmoid / relu head;
-    * ResnetFC as per-layer plain GEMMs on the saved activations, on hipBLASLt through
-      ``torch.matmul`` in fp32;
+    * ResnetFC as per-layer plain GEMMs on the saved activations (fp32 hipBLASLt via
+      ``torch.mm``);
     * ``pnr_points_input_backward`` for the input stage: the bilinear scatter into the
       channels-last latent (grid_sample backward), and dL/dz of every sample through the
       PE and the projection.
@@ -51,7 +51,10 @@ def _save_views(save, P, n_blocks, H=512):
 
 def mlp_backward(mlp, save, d_o, P):
     """ResnetFC backward (resnetfc.py:132-184, n_views == 1) given dL/d(pre-head output)
-    ``d_o`` (P, 4).  Returns ({param: grad}, d_feat (P, 64), d_zlat (P, 512) or None)."""
+    ``d_o`` (P, 4).  Returns ({param: grad}, d_feat (P, 64), d_zlat (P, 512) or None).
+    The 512-wide GEMMs are fp32 hipBLASLt GEMMs (split-fp16 GEMMs assembled from torch
+    ops measured 2x slower end to end: the split / scale passes cost more than they save)."""
+    mm = torch.mm
     nb = mlp.n_blocks
     lin_z = list(getattr(mlp, "lin_z", []))
     feat, z, slot = _save_views(save, P, nb)
@@ -66,17 +69,17 @@ def mlp_backward(mlp, save, d_o, P):
         blk = mlp.blocks[b]
         hb, xb = slot(nb + b), slot(b)
         w1, w0 = blk.fc_1.weight.detach(), blk.fc_0.weight.detach()
-        g[blk.fc_1.weight] = dx.t() @ hb
+        g[blk.fc_1.weight] = mm(dx.t(), hb)
         g[blk.fc_1.bias] = dx.sum(0)
-        dh = (dx @ w1) * (hb > 0)
-        g[blk.fc_0.weight] = dh.t() @ xb
+        dh = mm(dx, w1) * (hb > 0)
+        g[blk.fc_0.weight] = mm(dh.t(), xb)
         g[blk.fc_0.bias] = dh.sum(0)
-        dx = dx + (dh @ w0) * (xb > 0)
+        dx = dx + mm(dh, w0) * (xb > 0)
         if b < len(lin_z):
             lz = lin_z[b]
-            g[lz.weight] = dx.t() @ z
+            g[lz.weight] = mm(dx.t(), z)
             g[lz.bias] = dx.sum(0)
-            t = dx @ lz.weight.detach()
+            t = mm(dx, lz.weight.detach())
             dz = t if dz is None else dz + t
     d_in = mlp.lin_in.weight.shape[1]
     g[mlp.lin_in.weight] = dx.t() @ feat[:, :d_in]

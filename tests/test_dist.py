@@ -7,6 +7,7 @@ the max over ranks.
 """
 import os
 import socket
+import sys
 
 import pytest
 import torch
@@ -101,3 +102,65 @@ def test_two_rank_gloo_render_equals_single_process():
         assert p.exitcode == 0
     assert tmax == 2.0
     assert torch.equal(full, ref_rgb)
+
+
+# ---- data-parallel training: the gradient all-reduce -------------------
+def _train_grads(objs):
+    """Oracle training-step grads (tests/golden/train_step.npz inputs) over the objects
+    `objs` only: rays, streams, target, camera and latent rows of those objects."""
+    import fixtures
+    from oracle import ref_cpu
+
+    cfg, arr = fixtures.load("train_step")
+    per = arr["rays"].shape[1]
+    rows = torch.cat([torch.arange(o * per, (o + 1) * per) for o in objs])
+    sd = synth.pixelnerf_state(cfg["seed"], d_latent=cfg["d_latent"], d_hidden=cfg["d_hidden"])
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith("mlp_")}
+    sd.update(params)
+    latent = arr["latent"][objs].clone().requires_grad_(True)
+    scene = ref_cpu.Scene(latent, arr["poses"][objs], arr["focal"][objs], cfg["width"], cfg["height"],
+                          arr["c"][objs])
+
+    def model_fn(pts, coarse, dirs):
+        return ref_cpu.pixelnerf_forward(sd, scene, pts, coarse, dirs, d_latent=cfg["d_latent"])
+
+    streams = tuple(arr[k][rows] for k in ("u_coarse", "u_fine", "u_fine_jit", "n_depth"))
+    out = ref_cpu.render(model_fn, arr["rays"][objs], cfg["n_coarse"], cfg["n_fine"], cfg["n_fine_depth"],
+                         streams, cfg["white_bkgd"], depth_std=cfg["depth_std"])
+    mse = torch.nn.functional.mse_loss
+    loss = mse(out["coarse"]["rgb"], arr["target"][objs]) + mse(out["fine"]["rgb"], arr["target"][objs])
+    loss.backward()
+    return params
+
+
+def _train_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    torch.set_num_threads(1)
+    r, w, _ = pdist.init_from_env("gloo")
+    params = _train_grads([r])
+    n = pdist.allreduce_grads(list(params.values()), w, bucket_bytes=64 << 10)
+    if r == 0:
+        q.put(({k: p.grad.numpy().copy() for k, p in params.items()}, n))   # by value
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_gradient_allreduce_equals_full_batch():
+    """Each rank trains on its own object; the bucketed all-reduce (mean) of the rank
+    gradients equals the single-process gradient of the whole batch (equal shards)."""
+    ref = _train_grads([0, 1])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_train_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, n_coll = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert n_coll >= 2   # several buckets
+    for k, p in ref.items():
+        torch.testing.assert_close(torch.from_numpy(got[k]), p.grad, atol=1e-6, rtol=1e-4, msg=k)
