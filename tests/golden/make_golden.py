@@ -352,6 +352,34 @@ def train_case(name, *, d_hidden=32, d_latent=64, seed=21, rng_seed=6, sb=2, ray
     return cfg, arrays
 
 
+def frame_case(name, *, seed=1, size=32, rng_seed=8):
+    """gen_video.py:174-236 on one 32x32 frame: reference gen_rays -> render_par
+    (bind_parallel(simple_output=True)) -> fine rgb frame -> uint8 by truncation.
+    Shipped renderer conf (64 coarse + 32 fine incl. 16 depth, white background)."""
+    import util
+    from render import NeRFRenderer
+
+    sc = synth.scene_srn(seed=0, n_rays=1)
+    net = build_reference_net(512, 512, seed, sc["latent"], sc["poses"], sc["focal"], None,
+                              sc["width"], sc["height"])
+    renderer = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01,
+                            white_bkgd=True, eval_batch_size=100000)
+    render_par = renderer.bind_parallel(net, gpus=None, simple_output=True)
+    focal = torch.tensor(131.25 * size / 128.0)
+    rays = util.gen_rays(synth.srn_poses([40.0]), size, size, focal, 0.01, 4.0)   # (1, H, W, 8)
+    B = size * size
+    u_c, u_f, u_j, n_d = synth.rng_streams(rng_seed, B, 64, 32, 16)
+    with torch.no_grad(), injected_rng(u_c, u_f, u_j, n_d):
+        rgb, depth = render_par(rays.view(-1, 8)[None])
+    frames = rgb[0].view(-1, size, size, 3)
+    cfg = dict(name=name, seed=seed, size=size, rng_seed=rng_seed, latent_seed=sc["latent_seed"],
+               width=sc["width"], height=sc["height"])
+    return cfg, dict(rays=rays.numpy(), poses=sc["poses"].numpy(), focal=np.asarray(sc["focal"]),
+                     u_coarse=u_c.numpy(), u_fine=u_f.numpy(), u_fine_jit=u_j.numpy(),
+                     n_depth=n_d.numpy(), frames=frames.numpy(), depth=depth[0].numpy(),
+                     frames_u8=(frames.numpy() * 255).astype(np.uint8))
+
+
 def gen_rays_case(name):
     """util.gen_rays (util.py:238-276): (fx, fy) + principal point, and scalar focal with
     the default image-centre principal point."""
@@ -441,6 +469,8 @@ def main():
         save(*train_case("train_step"))
     if want("gen_rays"):
         save(*gen_rays_case("gen_rays"))
+    if want("frame32"):
+        save(*frame_case("frame32"))
     if want("fw_pointquery"):
         sc = synth.scene_srn(seed=0, n_rays=1)
         save(*point_query_case("fw_pointquery", seed=1, scene=sc, n_points=512))

@@ -376,3 +376,33 @@ def test_unsupported_config_fails_loudly():
                       torch.tensor(100.0, device=DEV), (64, 64))
     with torch.no_grad(), pytest.raises(NotImplementedError):
         net(torch.zeros(1, 4, 3, device=DEV), coarse=True, viewdirs=torch.zeros(1, 4, 3, device=DEV))
+
+
+# ------------------------------------------------------------- video frame --
+def test_frame_render_matches_reference_gen_video():
+    """gen_video.py:174-236 counterpart (pnr.video): one 32x32 frame through
+    render_par = bind_parallel(net, simple_output=True), shipped conf (64 + 32 incl. 16
+    depth), vs the reference's frame; uint8 frames equal except where rgb * 255 sits
+    within the fp32 tolerance of an integer (truncation boundary)."""
+    from pnr import video
+
+    cfg, arr = fixtures.load("frame32")
+    net = PixelNeRFNet(model_conf())
+    net.load_state_dict(synth.pixelnerf_state(cfg["seed"]), strict=False)
+    net = net.to(DEV).eval()
+    lat = synth.latent(cfg["latent_seed"], 1, 512, 64, 64)
+    net.encode_latent(lat.to(DEV), arr["poses"].to(DEV), arr["focal"].to(DEV), (cfg["width"], cfg["height"]))
+    r = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(DEV)
+    r.streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
+    render_par = r.bind_parallel(net, simple_output=True)
+    frames = video.render_frames(render_par, arr["rays"].to(DEV), ray_batch_size=cfg["size"] ** 2).cpu()
+    ref = arr["frames"]
+    assert frames.shape == ref.shape
+    ok = close_mask(frames, ref)
+    frac_bad = 1.0 - float(ok.float().mean())
+    assert frac_bad <= MAX_FLIP_FRAC, frac_bad   # searchsorted bin flips only
+    u8 = torch.from_numpy(video.to_uint8(frames)).int()
+    ref8 = arr["frames_u8"].int()
+    edge = ((ref * 255) - torch.round(ref * 255)).abs() <= 255 * (ATOL + RTOL)
+    diff = (u8 != ref8) & ok & ~edge
+    assert int(diff.sum()) == 0
