@@ -37,8 +37,14 @@ def env_rank():
 
 
 def init_from_env(backend="nccl"):
-    """torch.distributed over RCCL ("nccl" on ROCm) when WORLD_SIZE > 1."""
+    """torch.distributed over RCCL ("nccl" on ROCm) when WORLD_SIZE > 1.
+
+    Diagnostics only: PNR_DIST_BACKEND overrides the backend and PNR_FORCE_DEVICE pins every
+    rank to one device (rehearsing the multi-rank bench on a one-GPU box with gloo)."""
     rank, world, local = env_rank()
+    backend = os.environ.get("PNR_DIST_BACKEND", backend)
+    if "PNR_FORCE_DEVICE" in os.environ:
+        local = int(os.environ["PNR_FORCE_DEVICE"])
     if world > 1 and not dist.is_initialized():
         dist.init_process_group(backend, init_method="env://")
     return rank, world, local
@@ -48,6 +54,8 @@ def max_over_ranks(value, device=None):
     """Max of a float over all ranks (the timing reduction of bench.py)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return float(value)
+    if dist.get_backend() != "nccl":
+        device = "cpu"   # gloo: host tensor
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
