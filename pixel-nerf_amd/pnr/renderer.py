@@ -141,19 +141,22 @@ class NeRFRenderer(torch.nn.Module):
         B = rays.shape[0]
         if self.using_fine and self.n_fine <= 0:
             raise NotImplementedError("using_fine with n_fine = 0 (fine pass over coarse samples only)")
-        streams = self.draw_streams(B, rays.device)
         from .models import PixelNeRFNet
 
+        if isinstance(model, PixelNeRFNet) and torch.is_grad_enabled() and model.needs_grad():
+            return self._forward_train(model, rays, sb, want_weights)
+        streams = self.draw_streams(B, rays.device)
         if isinstance(model, PixelNeRFNet):
-            if torch.is_grad_enabled() and model.needs_grad():
-                return self._forward_train(model, rays, sb, streams, want_weights)
             return self._forward_fused(model, rays, sb, streams, want_weights)
         return self._forward_callback(model, rays, sb, streams, want_weights)
 
-    def _forward_train(self, net, rays, sb, streams, want_weights):
+    def _forward_train(self, net, rays, sb, want_weights):
         """The reference's autograd graph (nerf.py:251-303) over the HIP kernels
         (pnr/train.py): coarse pass, importance samples from the detached coarse weights
-        (nerf.py:130), depth samples with their gradient (nerf.py:150-161), sort, fine pass."""
+        (nerf.py:130), depth samples with their gradient (nerf.py:150-161), sort, fine pass.
+        With noise_std > 0 in training mode, sigma noise is added before compositing
+        (nerf.py:225-226) and the draws follow the reference's order: u_coarse, coarse
+        noise, u_fine, u_fine_jit, n_depth, fine noise."""
         from .train import Composite, RenderPoints, mlp_params
 
         r = net.hip_unsupported_reason()
@@ -163,22 +166,38 @@ class NeRFRenderer(torch.nn.Module):
             raise NotImplementedError("pnr: the training path implements one source view per object")
         if rays.device.type != "cuda":
             raise ValueError("pnr: rays must be on the HIP device")
-        if self.training and self.noise_std > 0.0:
-            raise NotImplementedError("noise_std > 0 in training mode is not implemented")
         kc = self.n_coarse
         kf = self.n_fine if self.using_fine else 0
         kfd = self.n_fine_depth if self.using_fine else 0
-        u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
+        noisy = self.training and self.noise_std > 0.0
+        B, dev = rays.shape[0], rays.device
+        lazy = noisy and self.streams is None   # draws interleave with the noise draws
+        if lazy:
+            u_c = torch.rand(B, kc, device=dev)
+        else:
+            u_c, u_f, u_j, n_d = [t.contiguous() for t in self.draw_streams(B, dev)]
+
+        def add_noise(raw):   # nerf.py:225-226 (sigma only; relu inside the composite)
+            if not noisy:
+                return raw
+            n = torch.randn(raw.shape[:2], device=dev)
+            return torch.cat([raw[..., :3], raw[..., 3:] + (n * self.noise_std).unsqueeze(-1)], -1)
+
         lat = net.encoder.latent_cl
         if net.stop_encoder_grad:
             lat = lat.detach()
         p_c = mlp_params(net.mlp_coarse)
         z_c = ops.sample_coarse(rays, kc, u_c, self.lindisp)
-        raw_c = RenderPoints.apply(net, True, rays, z_c, lat, *p_c)
-        w_c, rgb_c, d_c = Composite.apply(z_c, raw_c, rays, self.white_bkgd)
+        raw_c = add_noise(RenderPoints.apply(net, True, rays, z_c, lat, *p_c))
+        w_c, rgb_c, d_c = Composite.apply(z_c, raw_c.contiguous(), rays, self.white_bkgd)
         outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, d_c, sb, want_weights))
         if kf > 0:
             nf = kf - kfd
+            if lazy:
+                empty = torch.zeros(B, 0, device=dev)
+                u_f = torch.rand(B, nf, device=dev) if nf > 0 else empty
+                u_j = torch.rand(B, nf, device=dev) if nf > 0 else empty
+                n_d = torch.randn(B, kfd, device=dev) if kfd > 0 else empty
             with torch.no_grad():
                 z_ci = (ops.sample_fine(rays, z_c, w_c.detach(), d_c.detach(), nf, 0, self.depth_std, u_f, u_j,
                                         None, self.lindisp) if nf > 0 else z_c)
@@ -188,8 +207,8 @@ class NeRFRenderer(torch.nn.Module):
                 parts.append(torch.max(torch.min(z_d, rays[:, -1:]), rays[:, -2:-1]))
             z_f = torch.sort(torch.cat(parts, -1), -1)[0].contiguous()
             p_f = mlp_params(net.mlp_fine) if net.mlp_fine is not None else p_c
-            raw_f = RenderPoints.apply(net, False, rays, z_f, lat, *p_f)
-            w_f, rgb_f, d_f = Composite.apply(z_f, raw_f, rays, self.white_bkgd)
+            raw_f = add_noise(RenderPoints.apply(net, False, rays, z_f, lat, *p_f))
+            w_f, rgb_f, d_f = Composite.apply(z_f, raw_f.contiguous(), rays, self.white_bkgd)
             outputs.fine = self._pack_out(w_f, rgb_f, d_f, sb, want_weights)
         return outputs
 

@@ -103,3 +103,38 @@ def test_training_step_gradients_match_oracle(precision, tol):
         assert err <= tol * scale + 1e-9, "%s: max |d| %.3g vs max |ref| %.3g" % (k, err, scale)
     worst.sort()
     print("worst relative gradient error %.3g (%s)" % worst[-1])
+
+
+def test_training_noise_std_draw_order_matches_reference():
+    """noise_std > 0 in training mode (nerf.py:225-226): sigma noise per pass, with the
+    reference's draw order u_coarse, coarse noise, u_fine, u_fine_jit, n_depth, fine noise."""
+    cs = case(sb=1, rays_per_obj=4, kc=8, kf=6, kfd=2)
+    net = PixelNeRFNet(conf())
+    net.load_state_dict(cs["sd"], strict=False)
+    net = net.to(DEV)
+    lat = cs["latent"][:1].to(DEV).requires_grad_(True)
+    net.encode_latent(lat, cs["poses"][:1].to(DEV), cs["focal"][:1].to(DEV), (cs["width"], cs["height"]),
+                      c=cs["c"][:1].to(DEV), num_objs=1)
+    r = NeRFRenderer(n_coarse=8, n_fine=6, n_fine_depth=2, noise_std=0.5, white_bkgd=True).to(DEV).train()
+    log = []
+    rand, randn = torch.rand, torch.randn
+
+    def lrand(*s, **k):
+        log.append(("rand", tuple(s[0]) if isinstance(s[0], (tuple, list)) else tuple(s)))
+        return rand(*s, **k)
+
+    def lrandn(*s, **k):
+        log.append(("randn", tuple(s[0]) if isinstance(s[0], (tuple, list)) else tuple(s)))
+        return randn(*s, **k)
+
+    torch.rand, torch.randn = lrand, lrandn
+    try:
+        out = r(net, cs["rays"][:1].to(DEV), want_weights=True)
+    finally:
+        torch.rand, torch.randn = rand, randn
+    B = 4
+    assert log == [("rand", (B, 8)), ("randn", (B, 8)), ("rand", (B, 4)), ("rand", (B, 4)),
+                   ("randn", (B, 2)), ("randn", (B, 14))], log
+    loss = out.fine.rgb.sum() + out.coarse.rgb.sum()
+    loss.backward()
+    assert torch.isfinite(lat.grad).all()
