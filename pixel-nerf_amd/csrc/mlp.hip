@@ -192,19 +192,25 @@ __device__ __forceinline__ int scale_exp(float m) {
     int e = 14 - __builtin_amdgcn_frexp_expf(m);      // m < 2^frexp_exp
     return e < -64 ? -64 : (e > 40 ? 40 : e);
 }
-__global__ void k_layer_escale(PackSrc s, Layout L, float *__restrict__ out) {
-    const int layer = (int)blockIdx.x - 1;
+// pass 1: max |w| per layer (blockIdx.y = layer block as above), grid-strided over
+// blockIdx.x, combined with an integer atomicMax on the float bits (|w| >= 0) in the
+// header slot (zeroed by the host first)
+__global__ void k_layer_absmax(PackSrc s, Layout L, float *__restrict__ out) {
+    const int layer = (int)blockIdx.y - 1;
     const bool out_layer = layer == L.n_l512;
     const float *w = layer < 0 ? s.lin_in_w : (out_layer ? s.lin_out_w : s.w[layer]);
     const int64_t n = layer < 0 ? (int64_t)H * L.d_in : (out_layer ? (int64_t)L.d_out * H : (int64_t)H * H);
     float m = 0.f;
-    for (int64_t i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        m = fmaxf(m, fabsf(w[i]));
     m = wave_max(m);
-    __shared__ float red[4];
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0)
-        out[HDR_ESCALE + 1 + layer] = (float)scale_exp(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+    if ((threadIdx.x & 63) == 0)
+        atomicMax(reinterpret_cast<unsigned *>(out + HDR_ESCALE + blockIdx.y), __float_as_uint(m));
+}
+// pass 2: max -> scale exponent (as a float) in place
+__global__ void k_layer_escale(int n_slots, float *__restrict__ out) {
+    const int i = threadIdx.x;
+    if (i < n_slots) out[HDR_ESCALE + i] = (float)scale_exp(out[HDR_ESCALE + i]);
 }
 
 // One thread per (layer, k-step, row tile, lane): 8 weights w * 2^eW, each split
@@ -1227,8 +1233,12 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
     if (!launch_ok("mlp_pack")) return PNR_ERR_HIP;
     const int64_t n = (int64_t)(mlpk::KS32_IN + L.n_l512 * mlpk::KS32) * mlpk::NRT * 64;
     if (L.prec == PNR_PREC_F16X3) {
-        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3((unsigned)(2 + L.n_l512)), dim3(256), 0, st, s, L,
-                           static_cast<float *>(packed));
+        float *hdr = static_cast<float *>(packed);
+        if (hipMemsetAsync(hdr + mlpk::HDR_ESCALE, 0, sizeof(float) * (2 + L.n_l512), st) != hipSuccess)
+            return fail(PNR_ERR_HIP, "mlp_pack: hipMemsetAsync failed");
+        hipLaunchKernelGGL(mlpk::k_layer_absmax, dim3(32, (unsigned)(2 + L.n_l512)), dim3(256), 0, st, s, L, hdr);
+        if (!launch_ok("mlp_layer_absmax")) return PNR_ERR_HIP;
+        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3(1), dim3(64), 0, st, 2 + L.n_l512, hdr);
         if (!launch_ok("mlp_layer_escale")) return PNR_ERR_HIP;
         hipLaunchKernelGGL(mlpk::k_pack_f16, dim3((unsigned)((n + mlpk::KS32 * 64 + 255) / 256)), dim3(256), 0, st,
                            s, L, static_cast<float *>(packed));
