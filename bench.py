@@ -12,13 +12,20 @@ Multi-GPU (launched by torch.distributed.run): one process per GPU, every rank
 renders its own frame (a different target pose) — weak scaling, no data-path
 collective; a barrier + all_reduce(MAX) of the elapsed time bracket the region.
 
+The MLP arithmetic is --precision (default f16x3: fp32-accurate GEMMs from split-fp16
+products, include/pnr_abi.h); `dtype` stays "f32" (fp32 in / out / accumulation).
+
 The JSON line also carries
   roofline     — the dominant kernel (fine-pass fused point MLP, k_point_mlp):
-                 algorithmic FLOP per launch / its average duration measured with
+                 algorithmic fp32 FLOP per launch / its average duration measured with
                  HIP events recorded on the launch stream inside the timed region,
-                 against the fp32 MFMA peak (157.3 TFLOP/s);
+                 against the precision's fp32-equivalent MFMA peak (f16x3: 2500 / 3),
+                 plus the raw MFMA issue rate; `traffic` from the committed PMC pass;
   composite    — the standalone alpha-composite kernel's HBM roofline (bytes per
                  ray x rays / duration vs 8 TB/s) on a 1 M-ray batch;
+  extra_configs — cfg2 with the shipped conf, cfg3 (NMR 64x64) and cfg4 (DTU, 3 source
+                 views) on 1 GPU (informational; skip with --no-extra);
+  value_fp32_mfma — the same frame with the plain f32-MFMA arithmetic;
   cpu_baseline — the CPU oracle (oracle/ref_cpu.py, a restatement of the
                  reference's PyTorch path) on a bounded sample of the same frame,
                  timed on this host, rank 0 at N = 1 only.
@@ -171,6 +178,69 @@ def composite_roofline(dev, ev):
     return res
 
 
+def _time_render(net, renderer, rays, chunk, passes=2):
+    """Seconds per pass over `rays` (N, 8) in `chunk`-ray render_par calls (warm, synced)."""
+    render_par = renderer.bind_parallel(net, simple_output=True).eval()
+
+    def once():
+        for r in torch.split(rays, chunk, dim=0):
+            render_par(r[None])
+
+    with torch.no_grad():
+        once()
+        torch.cuda.synchronize(rays.device)
+        t0 = time.perf_counter()
+        for _ in range(passes):
+            once()
+        torch.cuda.synchronize(rays.device)
+    return (time.perf_counter() - t0) / passes
+
+
+def extra_configs(dev, precision):
+    """The other SURVEY §8(d) workloads on 1 GPU (informational, not `value`):
+    cfg2 with the shipped conf (64 + 32 incl. 16 depth samples), cfg3 NMR 64x64 (latent
+    32x32, 24 frames x 4096 rays), cfg4 DTU 400x300 with NS = 3 source views (one 120,000-
+    ray frame, the multi-view mean path), chunked as gen_video.py does (50,000 rays)."""
+    res = {}
+    sd = synth.pixelnerf_state(1)
+
+    def make(latent, poses, focal, size, c=None, n_obj=1):
+        net = PixelNeRFNet(model_conf())
+        net.load_state_dict(sd, strict=False)
+        net = net.to(dev).eval()
+        net.mlp_precision = precision
+        net.encode_latent(latent.to(dev), poses.to(dev), focal.to(dev), size,
+                          c=c.to(dev) if c is not None else None, num_objs=n_obj)
+        return net
+
+    # cfg2, shipped renderer conf
+    net = make(synth.latent(0, 1, 512, 64, 64), synth.srn_poses([0.0]), torch.tensor(131.25), (W, H))
+    rays = util.gen_rays(synth.srn_poses([30.0]).to(dev), W, H, torch.tensor(131.25), 0.01, 4.0).reshape(-1, 8)
+    r = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(dev)
+    s = _time_render(net, r, rays, CHUNK)
+    res["cfg2_shipped_64_32_16"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
+                                        gflop_per_ray=round(160 * FLOP_PER_POINT_NS1 / 1e9, 4))
+    # cfg3, NMR 64x64: 24 target views of one object
+    net = make(synth.latent(3, 1, 512, 32, 32), synth.srn_poses([0.0], radius=2.7), torch.tensor(70.0), (64, 64))
+    rays = util.gen_rays(synth.srn_poses([15.0 * i for i in range(24)], radius=2.7).to(dev), 64, 64,
+                         torch.tensor(70.0), 1.2, 4.0).reshape(-1, 8)
+    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True).to(dev)
+    s = _time_render(net, r, rays, 16384)
+    res["cfg3_nmr64_24frames"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_batch=round(s * 1e3, 3),
+                                      rays=int(rays.shape[0]))
+    # cfg4, DTU 400x300, 3 source views
+    sc = synth.scene_multiview(seed=8, n_views=3, n_rays=1)
+    net = make(synth.latent(8, 3, 512, 150, 200), sc["poses"][None], sc["focal"][None], (400, 300),
+               c=sc["c"][None])
+    rays = util.gen_rays(synth.srn_poses([10.0], phi=-12.0, radius=2.0).to(dev), 400, 300, sc["focal"],
+                         0.1, 5.0, c=sc["c"]).reshape(-1, 8)
+    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=False).to(dev)
+    s = _time_render(net, r, rays, 50000, passes=1)
+    res["cfg4_dtu_ns3_frame"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
+                                     gflop_per_ray=round(192 * (3 * 4761600 + 2101248) / 1e9, 4))
+    return res
+
+
 def pmc_traffic(kernel, render_pass):
     """Mean HBM bytes per launch of `kernel` in `render_pass` ("fine" / "coarse") from the
     newest committed PMC summary that has it (rocprofv3 counters cannot be read live from
@@ -198,6 +268,7 @@ def main():
     ap.add_argument("--cpu-rays", type=int, default=2048)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-composite", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the cfg2-shipped / cfg3 / cfg4 lines")
     ap.add_argument("--no-compare", action="store_true",
                     help="skip the f32-MFMA comparison frame (profiling runs)")
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
@@ -324,6 +395,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_composite:
         out["composite"] = composite_roofline(dev, ev)
+    if rank == 0 and world == 1 and not args.no_extra:
+        out["extra_configs"] = extra_configs(dev, args.precision)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(sd, rays.cpu(), args.cpu_rays)
     if rank == 0:

@@ -10,13 +10,13 @@ export TMPDIR=/tmp
 cd /tmp
 echo "== kernel trace"; date
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 $REPO/bench.py --steps 3 --warmup 1 --no-cpu --no-compare > $OUT/trace_bench.log 2>&1
+    python3 $REPO/bench.py --steps 3 --warmup 1 --no-cpu --no-compare --no-extra > $OUT/trace_bench.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 $OUT/trace_bench.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
 for ctr in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $ctr"; date
   timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_$ctr -o run -- \
-      python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu --no-compare > $OUT/pmc_$ctr.log 2>&1
+      python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu --no-compare --no-extra > $OUT/pmc_$ctr.log 2>&1
   rc=$?; echo "pmc $ctr rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done

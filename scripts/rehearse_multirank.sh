@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export PNR_DIST_BACKEND=gloo PNR_FORCE_DEVICE=0
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --no-composite --no-compare \
+    --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu --no-composite --no-compare --no-extra \
     > gpurun_out/rehearse_bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep metric gpurun_out/rehearse_bench.log | cut -c1-400
 [ $rc -eq 0 ] || exit $rc
