@@ -210,6 +210,17 @@ int pnr_gen_rays(const float *poses, int64_t n_images, int32_t pose_rows, int32_
                  int32_t height, float fx, float fy, float cx, float cy, float z_near,
                  float z_far, float *rays, pnr_stream_t stream);
 
+/* ---- encoder latent, channels-last --------------------------- */
+/* Replaces: the upsample + concat tail of SpatialEncoder.forward (encoder.py:150-160):
+ * n_maps (<= 8) trunk feature maps, maps[k] (n_images, channels[k], heights[k], widths[k])
+ * NCHW fp32 device pointers (the pointer arrays themselves are host memory), bilinearly
+ * upsampled with align_corners = True to (out_h, out_w) and concatenated along channels,
+ * written channels-LAST: latent_cl (n_images, out_h, out_w, sum channels). */
+int pnr_latent_channels_last(const float *const *maps, const int32_t *channels,
+                             const int32_t *heights, const int32_t *widths, int32_t n_maps,
+                             int32_t n_images, float *latent_cl, int32_t out_h, int32_t out_w,
+                             pnr_stream_t stream);
+
 /* ---- training (autograd over the ray march) ------------ */
 /* Floats of the activation save of pnr_render_points for n_points points:
  * per point features (64) | z (512) | relu(x) into fc_0 of each block (512 each) |

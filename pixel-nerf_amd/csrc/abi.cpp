@@ -24,6 +24,8 @@ int mlp_check_desc(const pnr_mlp_desc &);
 int mlp_pack(const pnr_mlp_weights &, void *, size_t, hipStream_t);
 size_t mlp_xsum_bytes(int ns);
 int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points);
+int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
+                     int, int, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
                          const float *, const float *, float *, float *, hipStream_t);
 int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, const float *, const float *,
@@ -328,6 +330,16 @@ int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n
     if (!z || !raw || !rays || !rgb || !depth) return fail(PNR_ERR_INVALID, "pnr_composite: NULL");
     if ((reinterpret_cast<uintptr_t>(raw) & 15) != 0) return fail(PNR_ERR_INVALID, "raw must be 16-byte aligned");
     return launch_composite(z, raw, rays, n_rays, k, white_bkgd, weights, rgb, depth, (hipStream_t)stream);
+}
+
+int pnr_latent_channels_last(const float *const *maps, const int32_t *channels, const int32_t *heights,
+                             const int32_t *widths, int32_t n_maps, int32_t n_images, float *latent_cl,
+                             int32_t out_h, int32_t out_w, pnr_stream_t stream) {
+    if (!maps || !channels || !heights || !widths || !latent_cl)
+        return fail(PNR_ERR_INVALID, "pnr_latent_channels_last: NULL");
+    if (n_images < 0 || out_h < 1 || out_w < 1) return fail(PNR_ERR_INVALID, "pnr_latent_channels_last: bad sizes");
+    return launch_latent_cl(maps, channels, heights, widths, n_maps, n_images, latent_cl, out_h, out_w,
+                            (hipStream_t)stream);
 }
 
 int pnr_gen_rays(const float *poses, int64_t n_images, int32_t pose_rows, int32_t width, int32_t height,

@@ -1,0 +1,84 @@
+// Encoder latent producer, channels-last.
+//
+// Replaces the tail of SpatialEncoder.forward (encoder.py:150-160): every trunk
+// feature map (conv1, layer1..layer3, NCHW) is bilinearly upsampled to the first map's
+// size (align_corners = True) and concatenated along channels.  The ray march consumes
+// the latent channels-LAST, so this kernel writes (N, H_l, W_l, sum C) directly: no
+// NCHW concat and no transpose copy.  Arithmetic as torch's CPU upsample_bilinear2d:
+//   scale = (in - 1) / (out - 1) (float), src = scale * dst, i0 = (int) src,
+//   l1 = src - i0, l0 = 1 - l1, i1 = i0 + (i0 < in - 1),
+//   out = l0h (l0w v00 + l1w v01) + l1h (l0w v10 + l1w v11)
+#include "pnr_common.h"
+
+namespace pnr {
+
+constexpr int MAX_MAPS = 8;
+
+struct LatentMaps {
+    const float *ptr[MAX_MAPS];
+    int c0[MAX_MAPS + 1];   // channel offset of each map in the output (c0[n_maps] = total)
+    int h[MAX_MAPS], w[MAX_MAPS];
+    int n_maps;
+};
+
+__device__ __forceinline__ void src_index(int in, int out, int dst, int &i0, int &i1, float &l0, float &l1) {
+    const float scale = out > 1 ? __fdiv_rn((float)(in - 1), (float)(out - 1)) : 0.f;
+    const float real = mul_rn(scale, (float)dst);
+    i0 = (int)real;
+    i1 = i0 + (i0 < in - 1 ? 1 : 0);
+    l1 = sub_rn(real, (float)i0);
+    l0 = sub_rn(1.f, l1);
+}
+
+__global__ __launch_bounds__(256) void k_latent_cl(LatentMaps m, int64_t n_out, int out_h, int out_w,
+                                                   float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_out) return;
+    const int C = m.c0[m.n_maps];
+    const int c = (int)(i % C);
+    const int64_t pix = i / C;
+    const int x = (int)(pix % out_w);
+    const int64_t t = pix / out_w;
+    const int y = (int)(t % out_h);
+    const int64_t n = t / out_h;
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < MAX_MAPS; ++j)
+        if (j < m.n_maps && c >= m.c0[j]) k = j;
+    const int cc = c - m.c0[k], hm = m.h[k], wm = m.w[k];
+    const int cm = m.c0[k + 1] - m.c0[k];
+    const float *src = m.ptr[k] + ((n * cm + cc) * (int64_t)hm) * wm;
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    src_index(hm, out_h, y, y0, y1, ly0, ly1);
+    src_index(wm, out_w, x, x0, x1, lx0, lx1);
+    const float v00 = src[(int64_t)y0 * wm + x0], v01 = src[(int64_t)y0 * wm + x1];
+    const float v10 = src[(int64_t)y1 * wm + x0], v11 = src[(int64_t)y1 * wm + x1];
+    const float top = add_rn(mul_rn(lx0, v00), mul_rn(lx1, v01));
+    const float bot = add_rn(mul_rn(lx0, v10), mul_rn(lx1, v11));
+    out[i] = add_rn(mul_rn(ly0, top), mul_rn(ly1, bot));
+}
+
+int launch_latent_cl(const float *const *maps, const int32_t *channels, const int32_t *heights,
+                     const int32_t *widths, int n_maps, int n_images, float *latent_cl, int out_h, int out_w,
+                     hipStream_t st) {
+    if (n_maps < 1 || n_maps > MAX_MAPS) return fail(PNR_ERR_UNSUPPORTED, "latent: 1..8 feature maps");
+    LatentMaps m = {};
+    m.n_maps = n_maps;
+    m.c0[0] = 0;
+    for (int k = 0; k < n_maps; ++k) {
+        if (!maps[k] || channels[k] < 1 || heights[k] < 1 || widths[k] < 1)
+            return fail(PNR_ERR_INVALID, "latent: bad feature map %d", k);
+        m.ptr[k] = maps[k];
+        m.h[k] = heights[k];
+        m.w[k] = widths[k];
+        m.c0[k + 1] = m.c0[k] + channels[k];
+    }
+    const int64_t n_out = (int64_t)n_images * out_h * out_w * m.c0[n_maps];
+    if (n_out == 0) return PNR_OK;
+    hipLaunchKernelGGL(k_latent_cl, dim3((unsigned)((n_out + 255) / 256)), dim3(256), 0, st, m, n_out, out_h,
+                       out_w, latent_cl);
+    return launch_ok("latent_cl") ? PNR_OK : PNR_ERR_HIP;
+}
+
+}  // namespace pnr

@@ -84,6 +84,8 @@ SIGNATURES = {
                                 c_vp, c_vp, c_i32, c_vp, c_vp]),
     "pnr_composite": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
     "pnr_gen_rays": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_f, c_f, c_f, c_f, c_f, c_f, c_vp, c_vp]),
+    "pnr_latent_channels_last": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32),
+                                         ctypes.POINTER(c_i32), c_i32, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "pnr_point_save_floats": (c_size, [ctypes.POINTER(MlpDesc), c_i64]),
     "pnr_render_points": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp,
                                   ctypes.POINTER(Rays), c_vp, c_i32, c_vp, c_vp, c_vp, c_size, c_vp]),

@@ -10,6 +10,7 @@ per scene and is not part of the per-ray hot path.
 
 The hot path consumes the latent channels-LAST; ``latent_cl`` keeps that copy.
 """
+import ctypes
 import warnings
 
 import torch
@@ -145,11 +146,39 @@ class SpatialEncoder(nn.Module):
         if self.num_layers > 4:
             x = m.layer4(x)
             latents.append(x)
+        if (x.is_cuda and not (torch.is_grad_enabled() and x.requires_grad)
+                and self.upsample_interp == "bilinear" and len(latents) <= 8):
+            return self.set_latent_maps(latents)
         size = latents[0].shape[-2:]
         for i in range(len(latents)):
             latents[i] = F.interpolate(latents[i], size, mode=self.upsample_interp,
                                        align_corners=True)
         return self.set_latent(torch.cat(latents, dim=1))
+
+    def set_latent_maps(self, maps):
+        """encoder.py:150-163 on the HIP device without the NCHW concat + transpose:
+        ``pnr_latent_channels_last`` upsamples (bilinear, align_corners) and concatenates
+        the trunk maps straight into the channels-last latent the ray march reads;
+        ``latent`` is its NCHW view (no copy)."""
+        from . import _lib
+
+        maps = [t.contiguous().float() for t in maps]
+        n, (h, w) = maps[0].shape[0], maps[0].shape[-2:]
+        c_total = sum(t.shape[1] for t in maps)
+        out = torch.empty(n, h, w, c_total, dtype=torch.float32, device=maps[0].device)
+        k = len(maps)
+        ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in maps])
+        ch = (ctypes.c_int32 * k)(*[t.shape[1] for t in maps])
+        hs = (ctypes.c_int32 * k)(*[t.shape[2] for t in maps])
+        ws = (ctypes.c_int32 * k)(*[t.shape[3] for t in maps])
+        _lib.check(_lib.load().pnr_latent_channels_last(ptrs, ch, hs, ws, k, n, _lib.ptr(out), h, w,
+                                                         _lib.stream_of(out.device)),
+                   "pnr_latent_channels_last")
+        self.latent = out.permute(0, 3, 1, 2)
+        ls = torch.tensor([w, h], dtype=torch.float32, device=out.device)
+        self.latent_scaling = ls / (ls - 1) * 2.0
+        self.latent_cl = out
+        return self.latent
 
     def index(self, uv, cam_z=None, image_size=(), z_bounds=None):
         """Bilinear feature lookup at image points (encoder.py:80-109); utility only —

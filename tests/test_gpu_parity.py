@@ -406,3 +406,37 @@ def test_frame_render_matches_reference_gen_video():
     edge = ((ref * 255) - torch.round(ref * 255)).abs() <= 255 * (ATOL + RTOL)
     diff = (u8 != ref8) & ok & ~edge
     assert int(diff.sum()) == 0
+
+
+# --------------------------------------------------------------- encoder --
+def test_latent_channels_last_matches_torch_upsample_concat():
+    """pnr_latent_channels_last (encoder.py:150-160 tail) vs the
+    reference's F.interpolate(bilinear, align_corners=True) + cat, transposed; and a no-grad
+    SpatialEncoder.forward on the device takes that path (latent_cl written directly)."""
+    import torch.nn.functional as F
+    from pnr.encoder import SpatialEncoder
+
+    g = torch.Generator().manual_seed(0)
+    n = 2
+    maps = [torch.randn(n, 64, 48, 56, generator=g), torch.randn(n, 64, 24, 28, generator=g),
+            torch.randn(n, 128, 12, 14, generator=g), torch.randn(n, 256, 6, 7, generator=g)]
+    ref = torch.cat([F.interpolate(t, (48, 56), mode="bilinear", align_corners=True) for t in maps], 1)
+    ref = ref.permute(0, 2, 3, 1).contiguous()
+    enc = SpatialEncoder(pretrained=False).to(DEV)
+    with torch.no_grad():
+        enc.set_latent_maps([t.to(DEV) for t in maps])
+    got = enc.latent_cl.cpu()
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got, ref, atol=1e-5, rtol=0)   # O(1) values: a few ulps
+    torch.testing.assert_close(enc.latent.cpu(), ref.permute(0, 3, 1, 2), atol=1e-5, rtol=0)
+    # full encoder forward on device under no_grad == the torch path of the same trunk
+    img = torch.rand(1, 3, 64, 64, generator=g).to(DEV) * 2 - 1
+    enc.eval()
+    with torch.no_grad():
+        lat_hip = enc(img).clone()
+        cl_hip = enc.latent_cl.clone()
+    lat_torch = enc(img.requires_grad_(True))   # grad-enabled input: the torch autograd path
+    # two separate trunk passes: MIOpen may choose different conv algorithms with / without
+    # grad, so the comparison carries the convolutions' own fp32 spread (upsample checked above)
+    torch.testing.assert_close(lat_hip, lat_torch.detach(), atol=1e-4, rtol=1e-5)
+    torch.testing.assert_close(cl_hip, enc.latent_cl.detach(), atol=1e-4, rtol=1e-5)
