@@ -251,6 +251,27 @@ int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, 
                               const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
                               const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream);
 
+/* Bytes of the transposed (backward) weight pack of an f16x3 model (precision
+ * PNR_PREC_F16X3); 0 for an invalid desc or another precision. */
+size_t pnr_mlp_packed_t_bytes(const pnr_mlp_desc *desc);
+
+/* Pack W^T of every 512-wide ResnetFC layer for pnr_mlp_backward.  `packed` is the model's
+ * pnr_mlp_pack output (same weights, same stream order): its header holds the scales. */
+int pnr_mlp_pack_t(const pnr_mlp_weights *w, const void *packed, void *packed_t, size_t packed_t_bytes,
+                   pnr_stream_t stream);
+
+/* Replaces: autograd of ResnetFC.forward (resnetfc.py:132-184, n_views == 1) up to the
+ * weight GEMMs, for an f16x3 model.  Given the forward's activation save (pnr_render_points)
+ * and d_o (n_points, 4) = dL / d lin_out output, writes the gradient of every layer's output:
+ *   dy ((2 n_blocks + 1), n_points, 512): [b] fc_0 of block b, [n_blocks] lin_in,
+ *       [n_blocks + 1 + b] fc_1 of block b; the lin_z of block b takes dy[n_blocks + b];
+ *   d_zlat (n_points, 512): dL / d (sampled latent), summed over the lin_z layers
+ *       (required when the model has lin_z layers).
+ * Weight and bias gradients are then dy^T . (saved layer input) and column sums of dy. */
+int pnr_mlp_backward(const pnr_mlp_desc *desc, const void *packed, const void *packed_t,
+                     const float *lin_out_w, const float *save, const float *d_o, int64_t n_points,
+                     float *dy, float *d_zlat, pnr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

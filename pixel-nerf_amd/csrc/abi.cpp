@@ -24,6 +24,10 @@ int mlp_check_desc(const pnr_mlp_desc &);
 int mlp_pack(const pnr_mlp_weights &, void *, size_t, hipStream_t);
 size_t mlp_xsum_bytes(int ns);
 int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points);
+size_t mlp_packed_t_bytes(const pnr_mlp_desc &);
+int mlp_pack_t(const pnr_mlp_weights &, const void *, void *, size_t, hipStream_t);
+int launch_mlp_bwd(const pnr_mlp_desc &, const void *, const void *, const float *, const float *, const float *,
+                   int64_t, float *, float *, hipStream_t);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
                      int, int, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
@@ -193,6 +197,30 @@ int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, 
                                 scene->latent, scene->latent_h, scene->latent_w, scene->image_w,
                                 scene->image_h, static_cast<const float *>(packed), desc->pe_n, d_feat,
                                 d_zlat, d_latent, d_z, (hipStream_t)stream);
+}
+
+size_t pnr_mlp_packed_t_bytes(const pnr_mlp_desc *desc) {
+    if (!desc) return 0;
+    return mlp_packed_t_bytes(*desc);
+}
+
+int pnr_mlp_pack_t(const pnr_mlp_weights *w, const void *packed, void *packed_t, size_t packed_t_bytes,
+                   pnr_stream_t stream) {
+    if (!w || !packed || !packed_t) return fail(PNR_ERR_INVALID, "pnr_mlp_pack_t: NULL argument");
+    return mlp_pack_t(*w, packed, packed_t, packed_t_bytes, (hipStream_t)stream);
+}
+
+int pnr_mlp_backward(const pnr_mlp_desc *desc, const void *packed, const void *packed_t, const float *lin_out_w,
+                     const float *save, const float *d_o, int64_t n_points, float *dy, float *d_zlat,
+                     pnr_stream_t stream) {
+    if (!desc || n_points < 0) return fail(PNR_ERR_INVALID, "pnr_mlp_backward: bad arguments");
+    if (n_points > 0 && (!packed || !packed_t || !lin_out_w || !save || !d_o || !dy))
+        return fail(PNR_ERR_INVALID, "pnr_mlp_backward: NULL argument");
+    if (((reinterpret_cast<uintptr_t>(lin_out_w) | reinterpret_cast<uintptr_t>(save) |
+          reinterpret_cast<uintptr_t>(d_o) | reinterpret_cast<uintptr_t>(dy) |
+          reinterpret_cast<uintptr_t>(d_zlat)) & 15) != 0)
+        return fail(PNR_ERR_INVALID, "pnr_mlp_backward: buffers must be 16-byte aligned");
+    return launch_mlp_bwd(*desc, packed, packed_t, lin_out_w, save, d_o, n_points, dy, d_zlat, (hipStream_t)stream);
 }
 
 // workspace layout of pnr_render_forward

@@ -262,6 +262,35 @@ __global__ void k_pack_f16(PackSrc s, Layout L, float *__restrict__ out) {
     }
 }
 
+// Backward (training) pack: W^T of every packed 512-wide layer in the k_pack_f16 fragment
+// layout, so that IN-gradient = W^T OUT-gradient runs on the forward's GEMM.  One thread
+// per (layer, k-step, row tile, lane): A[16 rt + (lane & 15)][32 ks + 8 (lane >> 4) + j] =
+// W[32 ks + 8 (lane >> 4) + j][16 rt + (lane & 15)] * 2^eW, eW from the forward pack's
+// header (max |W^T| = max |W|).  Output: n_l512 layers of layer_floats, no header.
+__global__ void k_pack_f16_t(PackSrc s, Layout L, const float *__restrict__ hdr, float *__restrict__ out) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t n_l = (int64_t)KS32 * NRT * 64;
+    if (t >= L.n_l512 * n_l) return;
+    const int layer = (int)(t / n_l);
+    const int64_t e = t % n_l;
+    const int ks = (int)(e / (NRT * 64)), rt = (int)((e / 64) % NRT), lane = (int)(e % 64);
+    float *dst = out + layer * L.layer_floats + (int64_t)ks * SKS16_FLOATS + rt * SRT16_FLOATS + lane * 4;
+    const int ew = (int)hdr[HDR_ESCALE + 1 + layer];
+    const int col = 16 * rt + (lane & 15);
+    typedef _Float16 h8t __attribute__((ext_vector_type(8)));
+    h8t p0, p1;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int row = 32 * ks + 8 * (lane >> 4) + j;
+        const float ws = __builtin_ldexpf(s.w[layer][(int64_t)row * H + col], ew);
+        const _Float16 h0 = (_Float16)ws;
+        p0[j] = h0;
+        p1[j] = (_Float16)(ws - (float)h0);
+    }
+    *reinterpret_cast<h8t *>(dst) = p0;
+    *reinterpret_cast<h8t *>(dst + 256) = p1;
+}
+
 // ------------------------------------------------------------------------------
 struct Args {
     const float *packed;
@@ -624,7 +653,8 @@ __device__ __forceinline__ void put_split4(_Float16 *P0, _Float16 *P1, int off, 
     *reinterpret_cast<u2 *>(P1 + off) = p1;
 }
 
-// relu(acc) of this wave's rows -> per-column partial maxima cmax[column][wave slot]
+// relu(acc) (RELU) or |acc| of this wave's rows -> per-column partial maxima cmax[column][wave slot]
+template <bool RELU = true>
 __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wave, int lane) {
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -632,7 +662,8 @@ __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wav
         float m = 0.f;
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
-            const f4 v = acc[r][c];
+            f4 v = acc[r][c];
+            if constexpr (!RELU) v = f4{fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
             m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
         }
         m = fmaxf(m, __shfl_xor(m, 16, 64));
@@ -644,8 +675,9 @@ __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wav
     }
 }
 
-// after relu_colmax + barrier: relu(acc) * 2^e_col split into P0 / P1 (this wave's rows),
-// e_col -> ecol[column]
+// after relu_colmax + barrier: relu(acc) (RELU) or acc, * 2^e_col split into P0 / P1 (this
+// wave's rows), e_col -> ecol[column]
+template <bool RELU = true>
 __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
                                                  const float *cmax, int *ecol, int wave, int lane) {
     const int g = lane >> 4, cl = lane & 15;
@@ -661,7 +693,7 @@ __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
-            const f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+            const f4 o = RELU ? f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)} : v;
             put_split4(P0, P1, col * ROWH + swz(col, 16 * (RTW * wave + r) + 4 * g), o, sc);
         }
     }
@@ -1165,6 +1197,165 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
 }
 
+// ---- training backward of ResnetFC (resnetfc.py:132-184, n_views == 1), PREC 3 -------------
+// Per 64-point tile, the input-gradient chain in reverse block order on the forward's GEMM
+// (W^T packed by k_pack_f16_t, the LDS image holding the signed gradient), with the relu
+// masks read from the forward's activation save:
+//   dx = (d_o W_out) . [x_f > 0]
+//   for b = nb-1 .. 0:  dY(fc_1 b) = dx
+//                       dh = (W_1^T dx) . [h_b > 0]              dY(fc_0 b) = dh
+//                       dx = dx + (W_0^T dh) . [x_b > 0]
+//                       b < n_linz:  dY(lin_z b) = dx,  dzlat += W_z^T dx
+//   dY(lin_in) = dx
+// The output gradients dY of every layer go to global memory for the weight gradients
+// (dW = dY^T IN over the points) and the bias gradients (column sums).  Slot order, chosen
+// so that those are strided batched GEMMs over the save's slots:
+//   dy[b] = dY(fc_0 b),  dy[nb] = dY(lin_in),  dy[nb + 1 + b] = dY(fc_1 b);
+//   dY(lin_z b) = dy[nb + b] (the same values).
+struct BwdArgs {
+    const float *hdr;        // forward pack (header: weight scale exponents)
+    const float *packed_t;   // k_pack_f16_t output
+    const float *w_out;      // lin_out weight (4 x 512, fp32)
+    const float *save;       // forward activation save (Args::save)
+    const float *d_o;        // (P, 4) gradient of the pre-head output
+    float *dy;               // (2 nb + 1) x P x 512
+    float *dzlat;            // (P, 512) gradient of the sampled latent (n_linz > 0)
+    Layout L;
+    int64_t n_points, n_tiles;
+};
+
+// this wave's rows of acc -> slot [point][512] (points < n_points)
+__device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
+                                           int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int64_t p = tile * COLS + 16 * c + cl;
+        if (p >= n_points) continue;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+            *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = acc[r][c];
+    }
+}
+// acc *= [saved activation > 0] (torch's relu backward); 0 past n_points
+__device__ __forceinline__ void relu_mask(Acc &acc, const float *slot, int64_t tile, int64_t n_points,
+                                          int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int64_t p = tile * COLS + 16 * c + cl;
+        const int64_t pc = p < n_points ? p : n_points - 1;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            const f4 m = *reinterpret_cast<const f4 *>(slot + pc * H + 16 * (RTW * wave + r) + 4 * g);
+            const f4 v = acc[r][c];
+            acc[r][c] = p < n_points ? f4{m.x > 0.f ? v.x : 0.f, m.y > 0.f ? v.y : 0.f,
+                                          m.z > 0.f ? v.z : 0.f, m.w > 0.f ? v.w : 0.f}
+                                     : f4{0.f, 0.f, 0.f, 0.f};
+        }
+    }
+}
+
+__global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, cl = lane & 15;
+    const Layout &L = a.L;
+    const int nb = L.n_blocks;
+    const int64_t P = a.n_points;
+    // LDS: P0 | P1 | cmax | ecol (as the forward's PREC 3 layout, no gather records)
+    _Float16 *P0 = reinterpret_cast<_Float16 *>(smem);
+    _Float16 *P1 = P0 + PART_HALVES;
+    float *cmax = reinterpret_cast<float *>(P1 + PART_HALVES);
+    int *ecol = reinterpret_cast<int *>(cmax + COLS * 8);
+    GemmCtx gc = {};
+    gc.ws_off = (int64_t)(RTW * wave) * SRT16_FLOATS + lane * 4;
+    gc.hdr = a.hdr;
+    gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
+    gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
+    gc.ecol = ecol;
+    gc.wave = wave;
+    gc.lane = lane;
+    const float *sv = a.save + P * (64 + H);   // relu slots after features and z
+    auto sv_slot = [&](int i) { return sv + P * H * i; };   // b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f
+    auto dy_slot = [&](int i) { return a.dy + P * H * i; };
+    auto publish = [&](const Acc &acc) {
+        __syncthreads();   // the previous image's readers are done
+        relu_colmax<false>(acc, cmax, wave, lane);
+        __syncthreads();
+        relu_store_split<false>(acc, P0, P1, cmax, ecol, wave, lane);
+        __syncthreads();
+    };
+    auto zero = [](Acc &acc) {
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+#pragma unroll
+            for (int c = 0; c < CT; ++c) acc[r][c] = f4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto layer = [&](int li) { return a.packed_t + (int64_t)li * L.layer_floats; };
+
+    Acc x, h;
+    for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        {   // dx = (d_o W_out) . [x_f > 0]
+            f4 wo[4][RTW];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int r = 0; r < RTW; ++r)
+                    wo[j][r] = *reinterpret_cast<const f4 *>(a.w_out + j * H + 16 * (RTW * wave + r) + 4 * g);
+#pragma unroll
+            for (int c = 0; c < CT; ++c) {
+                const int64_t p = tile * COLS + 16 * c + cl;
+                const f4 d = p < P ? *reinterpret_cast<const f4 *>(a.d_o + p * 4) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int r = 0; r < RTW; ++r)
+                    x[r][c] = ((d.x * wo[0][r] + d.y * wo[1][r]) + d.z * wo[2][r]) + d.w * wo[3][r];
+            }
+            relu_mask(x, sv_slot(2 * nb), tile, P, wave, lane);
+        }
+        bool published = false;
+        for (int b = nb - 1; b >= 0; --b) {
+            if (!published) publish(x);
+            store_rows(x, dy_slot(nb + 1 + b), tile, P, wave, lane);
+            const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
+            zero(h);
+            layer_gemm<3, NKB>(h, layer(l1), gc, 1 + l1);
+            relu_mask(h, sv_slot(nb + b), tile, P, wave, lane);
+            store_rows(h, dy_slot(b), tile, P, wave, lane);
+            publish(h);
+            zero(h);
+            layer_gemm<3, NKB>(h, layer(l0), gc, 1 + l0);
+            relu_mask(h, sv_slot(b), tile, P, wave, lane);
+#pragma unroll
+            for (int r = 0; r < RTW; ++r)
+#pragma unroll
+                for (int c = 0; c < CT; ++c) x[r][c] += h[r][c];
+            published = false;
+            if (b < L.n_linz) {
+                publish(x);
+                published = true;
+                const int lz = layer_index(b, 0, L.n_linz);
+                zero(h);
+                layer_gemm<3, NKB>(h, layer(lz), gc, 1 + lz);
+                const bool first = b == L.n_linz - 1;
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                    const int64_t p = tile * COLS + 16 * c + cl;
+                    if (p >= P) continue;
+#pragma unroll
+                    for (int r = 0; r < RTW; ++r) {
+                        f4 *q = reinterpret_cast<f4 *>(a.dzlat + p * H + 16 * (RTW * wave + r) + 4 * g);
+                        *q = first ? h[r][c] : *q + h[r][c];
+                    }
+                }
+            }
+        }
+        store_rows(x, dy_slot(nb), tile, P, wave, lane);
+    }
+}
+
 }  // namespace mlpk
 
 // ------------------------------------------------------------------------------
@@ -1204,13 +1395,9 @@ int mlp_check_desc(const pnr_mlp_desc &d) {
     return PNR_OK;
 }
 
-int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t st) {
+static int pack_src(const pnr_mlp_weights &w, const mlpk::Layout &L, mlpk::PackSrc &s) {
     const pnr_mlp_desc &d = w.desc;
-    int rc = mlp_check_desc(d);
-    if (rc) return rc;
-    mlpk::Layout L = mlpk::make_layout(d);
-    if (bytes < sizeof(float) * (size_t)L.total) return fail(PNR_ERR_WORKSPACE, "packed buffer too small");
-    mlpk::PackSrc s = {};
+    s = {};
     s.lin_in_w = w.lin_in_w; s.lin_in_b = w.lin_in_b;
     s.lin_out_w = w.lin_out_w; s.lin_out_b = w.lin_out_b;
     s.pe_f = w.pe_freqs; s.pe_p = w.pe_phases;
@@ -1227,6 +1414,17 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
             s.b[li] = bp;
         }
     }
+    return PNR_OK;
+}
+
+int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t st) {
+    const pnr_mlp_desc &d = w.desc;
+    int rc = mlp_check_desc(d);
+    if (rc) return rc;
+    mlpk::Layout L = mlpk::make_layout(d);
+    if (bytes < sizeof(float) * (size_t)L.total) return fail(PNR_ERR_WORKSPACE, "packed buffer too small");
+    mlpk::PackSrc s;
+    if ((rc = pack_src(w, L, s))) return rc;
     const int64_t blocks = (L.total + 255) / 256;
     hipLaunchKernelGGL(mlpk::k_pack, dim3((unsigned)blocks), dim3(256), 0, st, s, L,
                        static_cast<float *>(packed));
@@ -1249,6 +1447,56 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
         if (!launch_ok("mlp_pack_split")) return PNR_ERR_HIP;
     }
     return PNR_OK;
+}
+
+// ---- training backward (PREC 3) ----------------------------------------------------------
+size_t mlp_packed_t_bytes(const pnr_mlp_desc &d) {
+    if (mlp_check_desc(d) || d.precision != PNR_PREC_F16X3) return 0;
+    const mlpk::Layout L = mlpk::make_layout(d);
+    return sizeof(float) * (size_t)(L.n_l512 * L.layer_floats);
+}
+
+int mlp_pack_t(const pnr_mlp_weights &w, const void *packed, void *packed_t, size_t bytes, hipStream_t st) {
+    const pnr_mlp_desc &d = w.desc;
+    int rc = mlp_check_desc(d);
+    if (rc) return rc;
+    if (d.precision != PNR_PREC_F16X3)
+        return fail(PNR_ERR_UNSUPPORTED, "the fused MLP backward implements precision 3 (f16x3); got %d", d.precision);
+    const mlpk::Layout L = mlpk::make_layout(d);
+    if (bytes < mlp_packed_t_bytes(d)) return fail(PNR_ERR_WORKSPACE, "transposed pack buffer too small");
+    mlpk::PackSrc s;
+    if ((rc = pack_src(w, L, s))) return rc;
+    const int64_t n = (int64_t)L.n_l512 * mlpk::KS32 * mlpk::NRT * 64;
+    hipLaunchKernelGGL(mlpk::k_pack_f16_t, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s, L,
+                       static_cast<const float *>(packed), static_cast<float *>(packed_t));
+    return launch_ok("mlp_pack_t") ? PNR_OK : PNR_ERR_HIP;
+}
+
+int launch_mlp_bwd(const pnr_mlp_desc &d, const void *packed, const void *packed_t, const float *w_out,
+                   const float *save, const float *d_o, int64_t n_points, float *dy, float *dzlat, hipStream_t st) {
+    int rc = mlp_check_desc(d);
+    if (rc) return rc;
+    if (d.precision != PNR_PREC_F16X3)
+        return fail(PNR_ERR_UNSUPPORTED, "the fused MLP backward implements precision 3 (f16x3); got %d", d.precision);
+    mlpk::BwdArgs a = {};
+    a.L = mlpk::make_layout(d);
+    if (a.L.n_linz > 0 && !dzlat) return fail(PNR_ERR_INVALID, "mlp backward: d_zlat is required (n_linz > 0)");
+    if (n_points == 0) return PNR_OK;
+    a.hdr = static_cast<const float *>(packed);
+    a.packed_t = static_cast<const float *>(packed_t);
+    a.w_out = w_out;
+    a.save = save;
+    a.d_o = d_o;
+    a.dy = dy;
+    a.dzlat = dzlat;
+    a.n_points = n_points;
+    a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
+    const int cus = device_cu_count();
+    const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
+    // split image P0 + P1, column maxima, exponents = 137,472 B
+    const size_t lds = 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (mlpk::COLS * 8 + mlpk::COLS);
+    hipLaunchKernelGGL(mlpk::k_mlp_bwd, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
+    return launch_ok("mlp_bwd") ? PNR_OK : PNR_ERR_HIP;
 }
 
 int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points) {

@@ -141,21 +141,9 @@ class ResnetFC(nn.Module):
         return _lib.MlpDesc(self.d_in, self.d_latent, self.d_hidden, self.d_out, self.n_blocks,
                             self.combine_layer, pe_n, PRECISIONS[precision])
 
-    def packed(self, code, precision="fp32"):
-        """Packed fragment-order copy of the weights (re-packed when they change)."""
-        params = [p for p in self.parameters()] + [code._freqs, code._phases]
-        key = (precision,) + tuple((p.data_ptr(), p._version) for p in params)
-        cache = self.__dict__.get("_pnr_pack")
-        if cache is not None and cache[0] == key:
-            return cache[1], cache[2]
-        pe_n = int(code._freqs.numel())
-        desc = self.desc(pe_n, precision)
-        lib = _lib.load()
-        nbytes = lib.pnr_mlp_packed_bytes(desc)
-        if nbytes == 0:
-            _lib.check(-2, "pnr_mlp_packed_bytes")
-        dev = self.lin_out.weight.device
-        buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    def _weights(self, code, desc):
+        """pnr_mlp_weights over fp32 contiguous views of the parameters (+ the temporaries
+        that must outlive the pack launch)."""
         keep = []
 
         def p(t):
@@ -173,10 +161,52 @@ class ResnetFC(nn.Module):
             w.fc0_w[i], w.fc0_b[i] = p(blk.fc_0.weight), p(blk.fc_0.bias)
             w.fc1_w[i], w.fc1_b[i] = p(blk.fc_1.weight), p(blk.fc_1.bias)
         w.pe_freqs, w.pe_phases = p(code._freqs.reshape(-1)), p(code._phases.reshape(-1))
+        return w, keep
+
+    def _pack_key(self, code, precision):
+        params = [p for p in self.parameters()] + [code._freqs, code._phases]
+        return (precision,) + tuple((p.data_ptr(), p._version) for p in params)
+
+    def packed(self, code, precision="fp32"):
+        """Packed fragment-order copy of the weights (re-packed when they change).  The
+        pack is stream-ordered on the current stream: no host sync (the temporaries stay
+        referenced by the cache until the next re-pack)."""
+        key = self._pack_key(code, precision)
+        cache = self.__dict__.get("_pnr_pack")
+        if cache is not None and cache[0] == key:
+            return cache[1], cache[2]
+        pe_n = int(code._freqs.numel())
+        desc = self.desc(pe_n, precision)
+        lib = _lib.load()
+        nbytes = lib.pnr_mlp_packed_bytes(desc)
+        if nbytes == 0:
+            _lib.check(-2, "pnr_mlp_packed_bytes")
+        dev = self.lin_out.weight.device
+        buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        w, keep = self._weights(code, desc)
         _lib.check(lib.pnr_mlp_pack(w, _lib.ptr(buf), nbytes, _lib.stream_of(dev)), "pnr_mlp_pack")
-        torch.cuda.current_stream(dev).synchronize()  # `keep` temporaries may be freed after
-        self.__dict__["_pnr_pack"] = (key, desc, buf)
+        self.__dict__["_pnr_pack"] = (key, desc, buf, keep)
         return desc, buf
+
+    def packed_t(self, code, precision="f16x3"):
+        """Transposed (backward) pack for pnr_mlp_backward, f16x3 only: (desc, packed,
+        packed_t), re-packed with the forward pack."""
+        desc, buf = self.packed(code, precision)
+        key = self._pack_key(code, precision)
+        cache = self.__dict__.get("_pnr_pack_t")
+        if cache is not None and cache[0] == key:
+            return desc, buf, cache[1]
+        lib = _lib.load()
+        nbytes = lib.pnr_mlp_packed_t_bytes(desc)
+        if nbytes == 0:
+            _lib.check(-2, "pnr_mlp_packed_t_bytes (f16x3 models only)")
+        dev = self.lin_out.weight.device
+        buf_t = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        w, keep = self._weights(code, desc)
+        _lib.check(lib.pnr_mlp_pack_t(w, _lib.ptr(buf), _lib.ptr(buf_t), nbytes, _lib.stream_of(dev)),
+                   "pnr_mlp_pack_t")
+        self.__dict__["_pnr_pack_t"] = (key, buf_t, keep)
+        return desc, buf, buf_t
 
 
 def make_mlp(conf, d_in, d_latent=0, allow_empty=False, **kwargs):

@@ -89,6 +89,48 @@ def mlp_backward(mlp, save, d_o, P):
     return g, d_feat, dz
 
 
+def mlp_backward_fused(mlp, code, precision, save, d_o, P):
+    """``mlp_backward`` for f16x3 models: the input-gradient chain (masks, residual adds,
+    every 512-wide W^T GEMM, the summed latent gradient) runs in one ``pnr_mlp_backward``
+    launch on the forward's split-fp16 GEMM; the weight gradients are fp32 strided-batched
+    GEMMs over its per-layer output gradients and the activation save, and the bias
+    gradients one batched column sum."""
+    desc, packed, packed_t = mlp.packed_t(code, precision)
+    nb = mlp.n_blocks
+    lin_z = list(getattr(mlp, "lin_z", []))
+    feat, z, slot = _save_views(save, P, nb)
+    dev = d_o.device
+    d_o = d_o.contiguous()
+    dy = torch.empty(2 * nb + 1, P, 512, dtype=torch.float32, device=dev)
+    dzl = torch.empty(P, 512, dtype=torch.float32, device=dev) if lin_z else None
+    w_out = mlp.lin_out.weight.detach().float().contiguous()
+    lib = _lib.load()
+    _lib.check(lib.pnr_mlp_backward(desc, _lib.ptr(packed), _lib.ptr(packed_t), _lib.ptr(w_out), _lib.ptr(save),
+                                    _lib.ptr(d_o), P, _lib.ptr(dy), _lib.ptr(dzl), _lib.stream_of(dev)),
+               "pnr_mlp_backward")
+    g = {}
+    xf = slot(2 * nb)
+    g[mlp.lin_out.weight] = d_o.t() @ xf
+    g[mlp.lin_out.bias] = d_o.sum(0)
+    sums = dy.sum(1)
+    acts = save[P * (64 + 512): P * (64 + 512) + 2 * nb * P * 512].view(2 * nb, P, 512)
+    gw0 = torch.bmm(dy[:nb].transpose(1, 2), acts[:nb])        # fc_0: dY^T relu(x_b)
+    gw1 = torch.bmm(dy[nb + 1:].transpose(1, 2), acts[nb:])    # fc_1: dY^T relu(h_b)
+    for b, blk in enumerate(mlp.blocks):
+        g[blk.fc_0.weight], g[blk.fc_0.bias] = gw0[b], sums[b]
+        g[blk.fc_1.weight], g[blk.fc_1.bias] = gw1[b], sums[nb + 1 + b]
+    for b, lz in enumerate(lin_z):
+        g[lz.weight] = dy[nb + b].t() @ z
+        g[lz.bias] = sums[nb + b]
+    dx = dy[nb]
+    d_in = mlp.lin_in.weight.shape[1]
+    g[mlp.lin_in.weight] = dx.t() @ feat[:, :d_in]
+    g[mlp.lin_in.bias] = sums[nb]
+    d_feat = torch.zeros(P, 64, device=dev, dtype=torch.float32)
+    d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
+    return g, d_feat, dzl
+
+
 class RenderPoints(torch.autograd.Function):
     """raw (B, K, 4) = PixelNeRFNet at o + z d (models.py:146-266, via nerf.py:182-216),
     differentiable in z, the encoder latent (channels-last) and the MLP parameters."""
@@ -127,7 +169,10 @@ class RenderPoints(torch.autograd.Function):
         # head: [sigmoid(rgb), relu(sigma)] (models.py:258-265)
         d_o = torch.cat([d_out[:, :3] * out[:, :3] * (1.0 - out[:, :3]),
                          d_out[:, 3:] * (out[:, 3:] > 0)], dim=1)
-        g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P)
+        if net.mlp_precision == "f16x3":
+            g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P)
+        else:
+            g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P)
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         d_z = torch.empty(P, dtype=torch.float32, device=z.device) if need_z else None
         d_lat = torch.zeros_like(latent_cl) if need_lat else None

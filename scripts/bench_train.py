@@ -106,7 +106,9 @@ def main():
         "metric": "training rays/sec (cfg5: encoder + coarse/fine render + backward + grad all-reduce + Adam)",
         "value": round(rays_total / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "dtype": "f32", "arithmetic": args.precision + " forward, fp32 GEMM backward (pnr/train.py)",
+        "scaling": "weak", "dtype": "f32", "arithmetic": (args.precision + " forward + f16x3 fused input-gradient chain, fp32 weight GEMMs"
+                                                     if args.precision == "f16x3" else
+                                                     args.precision + " forward, fp32 GEMM backward") + " (pnr/train.py)",
         "data": "synthetic (random source images, hash-initialised MLPs, SRN geometry)",
         "config": {"workload": "cfg5: SB=%d objects x %d rays per rank, 64 coarse + 32 fine (16 depth)"
                                % (sb, per), "global_batch_rays": sb * per * world,
