@@ -272,6 +272,19 @@ int pnr_mlp_backward(const pnr_mlp_desc *desc, const void *packed, const void *p
                      const float *lin_out_w, const float *save, const float *d_o, int64_t n_points,
                      float *dy, float *d_zlat, pnr_stream_t stream);
 
+/* Workspace bytes of pnr_weight_grad (n_layers in 1..16); 0 if the sizes are invalid. */
+size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points);
+
+/* Replaces: the weight-gradient GEMMs autograd runs for the 512 x 512 nn.Linear layers of
+ * ResnetFC (resnetfc.py:132-184): for each layer j,
+ *   d_weight[j] (512 x 512, [out][in]) = dy[j]^T x[j],
+ * dy[j] (n_points x 512) the layer's output gradient (pnr_mlp_backward's slots), x[j]
+ * (n_points x 512) its input (the activation save).  dy, x, d_weight are host arrays of
+ * n_layers device pointers (16-byte aligned).  Split-bf16 products with fp32 accumulation
+ * (fp32-level error); deterministic (fixed reduction order). */
+int pnr_weight_grad(const float *const *dy, const float *const *x, float *const *d_weight, int32_t n_layers,
+                    int64_t n_points, void *workspace, size_t workspace_bytes, pnr_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

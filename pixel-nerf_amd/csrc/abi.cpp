@@ -28,6 +28,9 @@ size_t mlp_packed_t_bytes(const pnr_mlp_desc &);
 int mlp_pack_t(const pnr_mlp_weights &, const void *, void *, size_t, hipStream_t);
 int launch_mlp_bwd(const pnr_mlp_desc &, const void *, const void *, const float *, const float *, const float *,
                    int64_t, float *, float *, hipStream_t);
+size_t wgrad_workspace_bytes(int, int64_t);
+int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
+                 hipStream_t);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
                      int, int, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
@@ -221,6 +224,16 @@ int pnr_mlp_backward(const pnr_mlp_desc *desc, const void *packed, const void *p
           reinterpret_cast<uintptr_t>(d_zlat)) & 15) != 0)
         return fail(PNR_ERR_INVALID, "pnr_mlp_backward: buffers must be 16-byte aligned");
     return launch_mlp_bwd(*desc, packed, packed_t, lin_out_w, save, d_o, n_points, dy, d_zlat, (hipStream_t)stream);
+}
+
+size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points) {
+    return wgrad_workspace_bytes(n_layers, n_points);
+}
+
+int pnr_weight_grad(const float *const *dy, const float *const *x, float *const *d_weight, int32_t n_layers,
+                    int64_t n_points, void *workspace, size_t workspace_bytes, pnr_stream_t stream) {
+    if (!dy || !x || !d_weight) return fail(PNR_ERR_INVALID, "pnr_weight_grad: NULL argument");
+    return launch_wgrad(dy, x, d_weight, n_layers, n_points, workspace, workspace_bytes, (hipStream_t)stream);
 }
 
 // workspace layout of pnr_render_forward

@@ -381,33 +381,12 @@ __device__ __forceinline__ void gemm(Acc &acc, const float *__restrict__ wp, con
     }
 }
 
-typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef float f8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
-typedef unsigned u4 __attribute__((ext_vector_type(4)));
-
-// exact 3-way split x = x0 + x1 + x2 of 8 fp32 values into bf16 (RNE at each step).
-// Per pair: v_cvt_pk_bf16_f32, then the two halves back to fp32 by a shift / mask
-// (11 VALU per pair, no second conversion).
-__device__ __forceinline__ unsigned cvt_pk(float a, float b) {
-    bf2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, bf2);
-    return __builtin_bit_cast(unsigned, v);
-}
-// one pair (a, b) -> the packed bf16 pairs of its three parts
-__device__ __forceinline__ void split_pair(float a, float b, unsigned &p0, unsigned &p1, unsigned &p2) {
-    const unsigned h = cvt_pk(a, b);
-    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
-    const unsigned m = cvt_pk(ra, rb);
-    const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
-    p0 = h;
-    p1 = m;
-    p2 = cvt_pk(sa, sb);
-}
 __device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 &x1, bf8 &x2) {
     const float x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
 #ifdef PNR_ABLATE_SPLIT

@@ -28,7 +28,7 @@ import torch
 
 from . import _lib, ops
 
-__all__ = ["RenderPoints", "Composite", "mlp_backward", "mlp_params"]
+__all__ = ["RenderPoints", "Composite", "mlp_backward", "mlp_backward_fused", "weight_grad", "mlp_params"]
 
 
 def mlp_params(mlp):
@@ -89,12 +89,37 @@ def mlp_backward(mlp, save, d_o, P):
     return g, d_feat, dz
 
 
+def weight_grad(dys, xs, P):
+    """``pnr_weight_grad``: G[j] = dys[j]^T xs[j] (512 x 512) for (P, 512) fp32 matrices, in
+    one launch (split-bf16 products, fp32-level error, deterministic)."""
+    import ctypes
+
+    n = len(dys)
+    dev = dys[0].device
+    out = torch.empty(n, 512, 512, dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    wsb = lib.pnr_weight_grad_workspace_bytes(n, P)
+    if wsb == 0 and P > 0:
+        _lib.check(-1, "pnr_weight_grad_workspace_bytes")
+    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+
+    def arr(ts):
+        for t in ts:
+            assert t.is_contiguous() and t.shape == (P, 512) and t.dtype == torch.float32 and t.device == dev
+        return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
+
+    outs = (ctypes.c_void_p * n)(*[out[i].data_ptr() for i in range(n)])
+    _lib.check(lib.pnr_weight_grad(arr(dys), arr(xs), outs, n, P, _lib.ptr(ws), wsb, _lib.stream_of(dev)),
+               "pnr_weight_grad")
+    return out
+
+
 def mlp_backward_fused(mlp, code, precision, save, d_o, P):
     """``mlp_backward`` for f16x3 models: the input-gradient chain (masks, residual adds,
     every 512-wide W^T GEMM, the summed latent gradient) runs in one ``pnr_mlp_backward``
-    launch on the forward's split-fp16 GEMM; the weight gradients are fp32 strided-batched
-    GEMMs over its per-layer output gradients and the activation save, and the bias
-    gradients one batched column sum."""
+    launch on the forward's split-fp16 GEMM; the 512-wide weight gradients are one
+    ``pnr_weight_grad`` launch (split-bf16, fp32-level) over its per-layer output gradients
+    and the activation save, and the bias gradients one batched column sum."""
     desc, packed, packed_t = mlp.packed_t(code, precision)
     nb = mlp.n_blocks
     lin_z = list(getattr(mlp, "lin_z", []))
@@ -114,13 +139,16 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P):
     g[mlp.lin_out.bias] = d_o.sum(0)
     sums = dy.sum(1)
     acts = save[P * (64 + 512): P * (64 + 512) + 2 * nb * P * 512].view(2 * nb, P, 512)
-    gw0 = torch.bmm(dy[:nb].transpose(1, 2), acts[:nb])        # fc_0: dY^T relu(x_b)
-    gw1 = torch.bmm(dy[nb + 1:].transpose(1, 2), acts[nb:])    # fc_1: dY^T relu(h_b)
+    # one pnr_weight_grad launch: fc_0 (dY^T relu(x_b)), fc_1 (dY^T relu(h_b)), lin_z (dY^T z)
+    nz = len(lin_z)
+    gw = weight_grad([dy[b] for b in range(nb)] + [dy[nb + 1 + b] for b in range(nb)] +
+                     [dy[nb + b] for b in range(nz)],
+                     [acts[b] for b in range(nb)] + [acts[nb + b] for b in range(nb)] + [z] * nz, P)
     for b, blk in enumerate(mlp.blocks):
-        g[blk.fc_0.weight], g[blk.fc_0.bias] = gw0[b], sums[b]
-        g[blk.fc_1.weight], g[blk.fc_1.bias] = gw1[b], sums[nb + 1 + b]
+        g[blk.fc_0.weight], g[blk.fc_0.bias] = gw[b], sums[b]
+        g[blk.fc_1.weight], g[blk.fc_1.bias] = gw[nb + b], sums[nb + 1 + b]
     for b, lz in enumerate(lin_z):
-        g[lz.weight] = dy[nb + b].t() @ z
+        g[lz.weight] = gw[2 * nb + b]
         g[lz.bias] = sums[nb + b]
     dx = dy[nb]
     d_in = mlp.lin_in.weight.shape[1]

@@ -9,4 +9,8 @@ cd /tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -o run -- \
     python3 $REPO/scripts/bench_train.py --steps 3 --warmup 1 > $OUT/log.txt 2>&1
 rc=$?; echo "trace rc=$rc"; tail -2 $OUT/log.txt | cut -c1-300
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+# keep the stats and a one-step breakdown; the raw trace is too large to copy back
+python3 $REPO/scripts/train_step_breakdown.py $(find $OUT -name "*kernel_trace.csv" | head -1) 40 > $OUT/step_breakdown.txt
+find $OUT -name "*kernel_trace.csv" -delete
+head -25 $OUT/step_breakdown.txt

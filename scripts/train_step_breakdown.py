@@ -1,0 +1,33 @@
+"""Per-kernel time of the LAST training step in a rocprofv3 kernel trace of
+scripts/bench_train.py (the step after the last-but-one fine-MLP backward).
+Usage: python scripts/train_step_breakdown.py <run_kernel_trace.csv> [top]"""
+import collections
+import csv
+import sys
+
+
+def main():
+    rows = list(csv.DictReader(open(sys.argv[1])))
+    top = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # two MLP launches per step (coarse, fine); the backward kernel marks the step tail
+    marks = [i for i, r in enumerate(rows) if "k_mlp_bwd" in r["Kernel_Name"]]
+    if len(marks) < 4:
+        marks = [i for i, r in enumerate(rows) if "k_point_mlp" in r["Kernel_Name"]]
+    seg = rows[marks[-3] + 1: marks[-1] + 1]
+    t0, t1 = int(seg[0]["Start_Timestamp"]), int(seg[-1]["End_Timestamp"])
+    tot = collections.defaultdict(float)
+    cnt = collections.Counter()
+    for r in seg:
+        k = r["Kernel_Name"]
+        k = k[5:] if k.startswith("void ") else k
+        tot[k[:110]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        cnt[k[:110]] += 1
+    print("one step: span %.3f ms, kernel busy %.3f ms, %d dispatches" % ((t1 - t0) / 1e6, sum(tot.values()) / 1e6,
+                                                                        len(seg)))
+    for k, v in sorted(tot.items(), key=lambda x: -x[1])[:top]:
+        print("%8.3f ms %4d  %s" % (v / 1e6, cnt[k], k))
+
+
+if __name__ == "__main__":
+    main()
