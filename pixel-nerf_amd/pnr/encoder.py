@@ -17,6 +17,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .consts import device_const
+
 __all__ = ["SpatialEncoder", "resnet34_trunk"]
 
 
@@ -116,8 +118,7 @@ class SpatialEncoder(nn.Module):
     def set_latent(self, latent):
         """Install a feature map (NS, C, H_l, W_l) as forward() would (encoder.py:160-163)."""
         self.latent = latent
-        ls = torch.tensor([latent.shape[-1], latent.shape[-2]], dtype=torch.float32,
-                          device=latent.device)
+        ls = device_const((latent.shape[-1], latent.shape[-2]), latent.device)
         self.latent_scaling = ls / (ls - 1) * 2.0
         self.latent_cl = latent.permute(0, 2, 3, 1).contiguous()
         return latent
@@ -175,7 +176,7 @@ class SpatialEncoder(nn.Module):
                                                          _lib.stream_of(out.device)),
                    "pnr_latent_channels_last")
         self.latent = out.permute(0, 3, 1, 2)
-        ls = torch.tensor([w, h], dtype=torch.float32, device=out.device)
+        ls = device_const((w, h), out.device)
         self.latent_scaling = ls / (ls - 1) * 2.0
         self.latent_cl = out
         return self.latent

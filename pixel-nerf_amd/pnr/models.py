@@ -17,6 +17,7 @@ import torch
 from torch import nn
 
 from . import _lib
+from .consts import device_const
 from .conf import as_conf
 from .encoder import SpatialEncoder
 
@@ -303,7 +304,8 @@ class PixelNeRFNet(nn.Module):
         rot = poses[:, :3, :3].transpose(1, 2)
         trans = -torch.bmm(rot, poses[:, :3, 3:])
         self.poses = torch.cat((rot, trans), dim=-1)
-        self.image_shape = torch.tensor([float(width), float(height)], device=dev)
+        self.image_shape = device_const((width, height), dev)
+        self._image_wh = (float(width), float(height))   # host copy: hip_scene() never syncs
         focal = torch.as_tensor(focal).to(dev)
         if focal.dim() == 0:
             focal = focal[None, None].repeat((1, 2))
@@ -385,7 +387,10 @@ class PixelNeRFNet(nn.Module):
         sc.n_obj = self.num_objs
         sc.n_views = self.num_views_per_obj
         sc.latent_h, sc.latent_w, sc.latent_c = lat.shape[1], lat.shape[2], lat.shape[3]
-        sc.image_w, sc.image_h = float(self.image_shape[0]), float(self.image_shape[1])
+        wh = self.__dict__.get("_image_wh")
+        if wh is None:   # image_shape installed without _set_cameras (e.g. a state dict)
+            wh = (float(self.image_shape[0]), float(self.image_shape[1]))
+        sc.image_w, sc.image_h = wh
         return sc
 
     def hip_mlp(self, coarse):

@@ -49,6 +49,8 @@ def main():
     ap.add_argument("--sb", type=int, default=4)
     ap.add_argument("--rays-per-obj", type=int, default=256)
     ap.add_argument("--precision", default="f16x3")
+    ap.add_argument("--sync-debug", action="store_true",
+                    help="warn on every host-device synchronization inside the timed steps")
     args = ap.parse_args()
     rank, world, local = pdist.init_from_env("nccl")
     dev = torch.device("cuda", local)
@@ -95,8 +97,12 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    if args.sync_debug:
+        torch.cuda.set_sync_debug_mode("warn")
     for _ in range(args.steps):
         loss = step()
+    if args.sync_debug:
+        torch.cuda.set_sync_debug_mode("default")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -106,7 +112,7 @@ def main():
         "metric": "training rays/sec (cfg5: encoder + coarse/fine render + backward + grad all-reduce + Adam)",
         "value": round(rays_total / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-        "scaling": "weak", "dtype": "f32", "arithmetic": (args.precision + " forward + f16x3 fused input-gradient chain, fp32 weight GEMMs"
+        "scaling": "weak", "dtype": "f32", "arithmetic": (args.precision + " forward + f16x3 fused input-gradient chain + split-bf16 (x6) weight gradients"
                                                      if args.precision == "f16x3" else
                                                      args.precision + " forward, fp32 GEMM backward") + " (pnr/train.py)",
         "data": "synthetic (random source images, hash-initialised MLPs, SRN geometry)",
