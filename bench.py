@@ -28,7 +28,9 @@ The JSON line also carries
   value_fp32_mfma — the same frame with the plain f32-MFMA arithmetic;
   cpu_baseline — the CPU oracle (oracle/ref_cpu.py, a restatement of the
                  reference's PyTorch path) on a bounded sample of the same frame,
-                 timed on this host, rank 0 at N = 1 only.
+                 timed on this host, rank 0 at N = 1 only;
+  psnr_vs_reference_path — SURVEY §8(d)'s PSNR delta: the HIP render of that sample
+                 with the same injected random streams against the oracle's render.
 """
 import argparse
 import ctypes
@@ -131,12 +133,49 @@ def cpu_baseline(sd, rays_cpu, n_rays):
     with torch.no_grad():
         ref_cpu.render(fn, rays[:, :8], KC, KF, 0, tuple(s[:8] for s in streams), True)  # warm-up
         t0 = time.perf_counter()
-        ref_cpu.render(fn, rays, KC, KF, 0, streams, True)
+        ref = ref_cpu.render(fn, rays, KC, KF, 0, streams, True)
         dt = time.perf_counter() - t0
     return dict(value=round(n_rays / dt, 2), unit="rays/s", cores=torch.get_num_threads(),
                 kind="port",
                 sample="%d rays of the cfg2 frame x (64+64) samples, oracle/ref_cpu.py, %.1f s" % (
-                    n_rays, dt))
+                    n_rays, dt)), ref, streams
+
+
+def psnr_vs_reference_path(net, rays_dev, ref, streams, dev):
+    """SURVEY §8(d)'s PSNR delta: the HIP render of the cpu_baseline rays with the SAME
+    injected random streams, against the oracle's render of them (oracle/ref_cpu.py, the
+    CPU restatement pinned to the reference).  `agreement_db` = PSNR(HIP, oracle);
+    `delta_db` = PSNR(HIP, target) - PSNR(oracle, target) for a seeded U(0,1) target image
+    (no ground-truth frames offline)."""
+    n = rays_dev.shape[0]
+    r = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True).to(dev)
+    r.streams = tuple(t.to(dev) for t in streams)
+    with torch.no_grad():
+        out = r(net, rays_dev[None].contiguous())
+    tgt = torch.from_numpy(synth.hash_uniform(5, n * 3).astype("float32")).reshape(n, 3)
+
+    def psnr(a, b):   # util.psnr (util.py:474-481), +inf for identical images
+        return float("inf") if float(((a - b) ** 2).mean()) == 0.0 else float(util.psnr(a, b))
+
+    res = {}
+    for name in ("coarse", "fine"):
+        mine = getattr(out, name).rgb[0].float().cpu()
+        theirs = ref[name]["rgb"][0].float()
+        agree = psnr(mine, theirs)
+        # SURVEY §8(c): rays whose fine-bin choice (inverse-CDF sample, a4) differs under
+        # fp32-level weight differences are reported and excluded from the second figure
+        flip = (mine - theirs).abs().amax(-1) > 1e-4
+        keep = ~flip
+        agree_kept = psnr(mine[keep], theirs[keep]) if bool(keep.any()) else float("inf")
+        res[name] = dict(agreement_db=round(agree, 2) if agree < float("inf") else None,
+                         delta_db=round(psnr(mine, tgt) - psnr(theirs, tgt), 6),
+                         max_abs_rgb=float((mine - theirs).abs().max()),
+                         bin_flip_rays=int(flip.sum()),
+                         agreement_db_excl_flips=round(agree_kept, 2) if agree_kept < float("inf") else None,
+                         max_abs_rgb_excl_flips=float((mine[keep] - theirs[keep]).abs().max())
+                         if bool(keep.any()) else 0.0)
+    res["rays"] = n
+    return res
 
 
 def composite_roofline(dev, ev):
@@ -398,7 +437,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_extra:
         out["extra_configs"] = extra_configs(dev, args.precision)
     if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(sd, rays.cpu(), args.cpu_rays)
+        out["cpu_baseline"], ref, streams = cpu_baseline(sd, rays.cpu(), args.cpu_rays)
+        out["psnr_vs_reference_path"] = psnr_vs_reference_path(net, rays[:args.cpu_rays], ref, streams, dev)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
