@@ -104,15 +104,17 @@ __device__ __forceinline__ unsigned cvt_pk(float a, float b) {
     bf2 v = __builtin_convertvector((float __attribute__((ext_vector_type(2)))){a, b}, bf2);
     return __builtin_bit_cast(unsigned, v);
 }
-// one pair (a, b) -> the packed bf16 pairs of its three parts
+// one pair (a, b) -> the packed bf16 pairs of its three parts (the pair's subtractions as
+// one packed fp32 op, v_pk_add_f32: same per-element RNE rounding)
 __device__ __forceinline__ void split_pair(float a, float b, unsigned &p0, unsigned &p1, unsigned &p2) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
     const unsigned h = cvt_pk(a, b);
-    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
-    const unsigned m = cvt_pk(ra, rb);
-    const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
+    const f2v r = f2v{a, b} - f2v{__uint_as_float(h << 16), __uint_as_float(h & 0xffff0000u)};
+    const unsigned m = cvt_pk(r.x, r.y);
+    const f2v t = r - f2v{__uint_as_float(m << 16), __uint_as_float(m & 0xffff0000u)};
     p0 = h;
     p1 = m;
-    p2 = cvt_pk(sa, sb);
+    p2 = cvt_pk(t.x, t.y);
 }
 
 }  // namespace pnr

@@ -1,9 +1,10 @@
 #!/usr/bin/env python
 """Derived PMC metrics of the k_point_mlp launches from scripts/counters.sh output.
 
-Usage: python scripts/analyze_counters.py gpurun_out/ctr_<tag>
-Per render pass (coarse / fine, told apart by launch order within each probe chunk:
-coarse MLP first, then fine) prints the mean over launches of:
+Usage: python scripts/analyze_counters.py gpurun_out/ctr_<tag> [kernel substring]
+For k_point_mlp (default) per render pass (coarse / fine, told apart by launch order within
+each probe chunk: coarse MLP first, then fine), for any other kernel over all its launches,
+prints the mean over launches of:
   clock_ghz      GRBM_GUI_ACTIVE / XCDs / duration
   mfma_busy      SQ_VALU_MFMA_BUSY_CYCLES / (CUs * 4 SIMDs * clock cycles)
   wait_any, wait_inst, active_inst   SQ_WAIT_ANY / SQ_WAIT_INST_ANY / SQ_ACTIVE_INST_ANY
@@ -20,13 +21,13 @@ from collections import defaultdict
 CUS, XCDS = 256, 8
 
 
-def load(d):
+def load(d, kernel="k_point_mlp"):
     per = defaultdict(dict)   # dispatch id -> {counter: value, "name", "dur"}
     for path in glob.glob(os.path.join(d, "g*", "run_counter_collection.csv")):
         grp = os.path.basename(os.path.dirname(path))
         with open(path) as f:
             for r in csv.DictReader(f):
-                if "k_point_mlp" not in r["Kernel_Name"]:
+                if kernel not in r["Kernel_Name"]:
                     continue
                 key = (grp, int(r["Dispatch_Id"]))
                 e = per[key]
@@ -39,7 +40,8 @@ def load(d):
         ids = sorted(k[1] for k in per if k[0] == grp)
         for i, did in enumerate(ids):
             e = per[(grp, did)]
-            label = "%s %s" % (e["name"], "coarse" if i % 2 == 0 else "fine")
+            label = ("%s %s" % (e["name"], "coarse" if i % 2 == 0 else "fine")
+                     if kernel == "k_point_mlp" else e["name"])
             for k, v in e.items():
                 if k != "name":
                     out[label][k].append(v)
@@ -51,7 +53,7 @@ def mean(v):
 
 
 def main():
-    res = load(sys.argv[1])
+    res = load(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "k_point_mlp")
     for label, c in sorted(res.items()):
         m = {k: mean(v) for k, v in c.items()}
         line = [label, "dur %.3f ms" % (m["dur"] * 1e3)]

@@ -1,8 +1,10 @@
 #!/bin/bash
-# PMC passes over scripts/mlp_probe.py (one rocprofv3 run per counter group).
+# PMC passes over a probe script (default scripts/mlp_probe.py; one rocprofv3 run per
+# counter group).  Usage: counters.sh <tag> [probe.py]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/ctr_${1:-x}
+PROBE=$REPO/${2:-scripts/mlp_probe.py}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
@@ -11,6 +13,6 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
            "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_SALU TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/g$i -o run -- python3 $REPO/scripts/mlp_probe.py > $OUT/g$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/g$i -o run -- python3 $PROBE > $OUT/g$i.log 2>&1
   rc=$?; echo "group $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/g$i.log; exit $rc; }
 done
