@@ -224,7 +224,10 @@ int pnr_latent_channels_last(const float *const *maps, const int32_t *channels,
 /* ---- training (autograd over the ray march) ------------ */
 /* Floats of the activation save of pnr_render_points for n_points points:
  * per point features (64) | z (512) | relu(x) into fc_0 of each block (512 each) |
- * relu(h) of each block (512 each) | relu(x) into lin_out (512), each region [point][width]. */
+ * relu(h) of each block (512 each) | relu(x) into lin_out (512), each region [point][width],
+ * then the relu sign masks of the 2 n_blocks + 1 relu regions (same order), each
+ * [point][64 bytes], [activation n > 0] of n = 64 w + 16 r + 4 g + e (w, r, g, e =
+ * 0..7, 0..3, 0..3, 0..3) at bit 4 (r & 1) + e of byte 8 w + 2 g + (r >> 1). */
 size_t pnr_point_save_floats(const pnr_mlp_desc *desc, int64_t n_points);
 
 /* Replaces: the model call of NeRFRenderer.composite (nerf.py:182-216) under autograd:

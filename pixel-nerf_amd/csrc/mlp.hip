@@ -316,9 +316,14 @@ struct Args {
     float *save;
 };
 
-// floats of the activation save per point (Args::save)
+// floats of the activation save per point (Args::save): the fp32 regions, then the relu
+// sign masks of the 2 nb + 1 relu slots, [slot][point][64 bytes] (save_mask's bit order)
+// for the backward's masks
 __host__ __device__ constexpr int64_t save_floats_per_point(int n_blocks) {
-    return 64 + (int64_t)H * (2 + 2 * n_blocks);
+    return 64 + (int64_t)H * (2 + 2 * n_blocks) + 16 * (2 * n_blocks + 1);
+}
+__host__ __device__ constexpr int64_t save_mask_offset(int n_blocks, int64_t n_points) {
+    return (64 + (int64_t)H * (2 + 2 * n_blocks)) * n_points;
 }
 
 
@@ -342,6 +347,26 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) =
                 f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
         }
+    }
+}
+
+// [acc > 0] of this wave's rows -> mask slot [point][64 bytes].  Byte 8 wave + 2g + w of a
+// point holds rows 16 (RTW wave + r) + 4g + e, r = 2w + h, at bit 4h + e: a lane's 16 bits
+// are one contiguous 2-byte store per point, and a wave's 64 rows are one 8-byte word pair.
+__device__ __forceinline__ void save_mask(const Acc &acc, uint32_t *mslot, int64_t tile, int64_t n_points,
+                                          int wave, int lane) {
+    static_assert(RTW == 4, "mask bytes assume 4 row tiles per wave");
+    const int g = lane >> 4, cl = lane & 15;
+    auto nib = [](const f4 &v) {
+        return (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) | (v.w > 0.f ? 8u : 0u);
+    };
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int64_t p = tile * COLS + 16 * c + cl;
+        const uint32_t bits = nib(acc[0][c]) | (nib(acc[1][c]) << 4) | (nib(acc[2][c]) << 8) | (nib(acc[3][c]) << 12);
+        if (p < n_points)
+            *reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(mslot) + p * 64 + 8 * wave + 2 * g) =
+                (uint16_t)bits;
     }
 }
 
@@ -836,8 +861,12 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     const int64_t P = a.n_points;
     float *sv_f = a.save, *sv_z = a.save ? a.save + P * 64 : nullptr;
     auto sv_slot = [&](int i) { return sv_z + P * H * (1 + i); };   // i: block b -> x_in, nb + b -> h, 2nb -> x_f
+    uint32_t *sv_mask = a.save ? reinterpret_cast<uint32_t *>(a.save + save_mask_offset(L.n_blocks, P)) : nullptr;
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx) {
-        if (a.save) save_relu(acc, sv_slot(save_idx), tile, P, wave, lane);
+        if (a.save) {
+            save_relu(acc, sv_slot(save_idx), tile, P, wave, lane);
+            save_mask(acc, sv_mask + P * 16 * save_idx, tile, P, wave, lane);
+        }
 #ifdef PNR_GEMM_ONLY
         {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
             float t = 0.f;
@@ -1180,7 +1209,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 // Per 64-point tile, the input-gradient chain in reverse block order on the forward's GEMM
 // (W^T packed by k_pack_f16_t, the LDS image holding the signed gradient), with the relu
 // masks read from the forward's activation save:
-//   dx = (d_o W_out) . [x_f > 0]
+//   dx = (d_o W_out) . [x_f > 0]       (masks: the forward's sign bits, save_mask)
 //   for b = nb-1 .. 0:  dY(fc_1 b) = dx
 //                       dh = (W_1^T dx) . [h_b > 0]              dY(fc_0 b) = dh
 //                       dx = dx + (W_0^T dh) . [x_b > 0]
@@ -1216,21 +1245,34 @@ __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t 
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = acc[r][c];
     }
 }
-// acc *= [saved activation > 0] (torch's relu backward); 0 past n_points
-__device__ __forceinline__ void relu_mask(Acc &acc, const float *slot, int64_t tile, int64_t n_points,
+// relu backward masks from the forward's sign bits (save_mask): this lane's two words of
+// each of its CT points, loaded before the GEMM whose output they mask
+typedef unsigned u2m __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void load_mask(u2m (&mk)[CT], const uint32_t *mslot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
-    const int g = lane >> 4, cl = lane & 15;
+    const int cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
         const int64_t pc = p < n_points ? p : n_points - 1;
+        mk[c] = *reinterpret_cast<const u2m *>(mslot + pc * 16 + 2 * wave);
+    }
+}
+// acc *= [activation > 0] (torch's relu backward); 0 past n_points
+__device__ __forceinline__ void relu_mask(Acc &acc, const u2m (&mk)[CT], int64_t tile, int64_t n_points,
+                                          int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const bool valid = tile * COLS + 16 * c + cl < n_points;
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
-            const f4 m = *reinterpret_cast<const f4 *>(slot + pc * H + 16 * (RTW * wave + r) + 4 * g);
+            // byte 2g + (r >> 1) of the wave's 8 bytes, bit 4 (r & 1) + e
+            const int byte = 2 * g + (r >> 1);
+            const uint32_t nib = valid ? (byte >= 4 ? mk[c].y : mk[c].x) >> (8 * (byte & 3) + 4 * (r & 1)) : 0u;
             const f4 v = acc[r][c];
-            acc[r][c] = p < n_points ? f4{m.x > 0.f ? v.x : 0.f, m.y > 0.f ? v.y : 0.f,
-                                          m.z > 0.f ? v.z : 0.f, m.w > 0.f ? v.w : 0.f}
-                                     : f4{0.f, 0.f, 0.f, 0.f};
+            acc[r][c] = f4{(nib & 1u) ? v.x : 0.f, (nib & 2u) ? v.y : 0.f, (nib & 4u) ? v.z : 0.f,
+                           (nib & 8u) ? v.w : 0.f};
         }
     }
 }
@@ -1257,8 +1299,10 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     gc.ecol = ecol;
     gc.wave = wave;
     gc.lane = lane;
-    const float *sv = a.save + P * (64 + H);   // relu slots after features and z
-    auto sv_slot = [&](int i) { return sv + P * H * i; };   // b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f
+    // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f
+    const uint32_t *msk = reinterpret_cast<const uint32_t *>(a.save + save_mask_offset(nb, P));
+    auto mask_slot = [&](int i) { return msk + P * 16 * i; };
+    u2m mk[CT];
     auto dy_slot = [&](int i) { return a.dy + P * H * i; };
     auto publish = [&](const Acc &acc) {
         __syncthreads();   // the previous image's readers are done
@@ -1278,6 +1322,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     Acc x, h;
     for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         {   // dx = (d_o W_out) . [x_f > 0]
+            load_mask(mk, mask_slot(2 * nb), tile, P, wave, lane);
             f4 wo[4][RTW];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -1292,7 +1337,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                 for (int r = 0; r < RTW; ++r)
                     x[r][c] = ((d.x * wo[0][r] + d.y * wo[1][r]) + d.z * wo[2][r]) + d.w * wo[3][r];
             }
-            relu_mask(x, sv_slot(2 * nb), tile, P, wave, lane);
+            relu_mask(x, mk, tile, P, lane);
         }
         bool published = false;
         for (int b = nb - 1; b >= 0; --b) {
@@ -1300,13 +1345,15 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
             store_rows(x, dy_slot(nb + 1 + b), tile, P, wave, lane);
             const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
             zero(h);
+            load_mask(mk, mask_slot(nb + b), tile, P, wave, lane);   // lands during the GEMM
             layer_gemm<3, NKB>(h, layer(l1), gc, 1 + l1);
-            relu_mask(h, sv_slot(nb + b), tile, P, wave, lane);
+            relu_mask(h, mk, tile, P, lane);
             store_rows(h, dy_slot(b), tile, P, wave, lane);
             publish(h);
             zero(h);
+            load_mask(mk, mask_slot(b), tile, P, wave, lane);
             layer_gemm<3, NKB>(h, layer(l0), gc, 1 + l0);
-            relu_mask(h, sv_slot(b), tile, P, wave, lane);
+            relu_mask(h, mk, tile, P, lane);
 #pragma unroll
             for (int r = 0; r < RTW; ++r)
 #pragma unroll

@@ -13,4 +13,4 @@ rc=$?; echo "trace rc=$rc"; tail -2 $OUT/log.txt | cut -c1-300
 # keep the stats and a one-step breakdown; the raw trace is too large to copy back
 python3 $REPO/scripts/train_step_breakdown.py $(find $OUT -name "*kernel_trace.csv" | head -1) 40 > $OUT/step_breakdown.txt
 find $OUT -name "*kernel_trace.csv" -delete
-head -25 $OUT/step_breakdown.txt
+head -60 $OUT/step_breakdown.txt

@@ -27,6 +27,18 @@ def main():
                                                                         len(seg)))
     for k, v in sorted(tot.items(), key=lambda x: -x[1])[:top]:
         print("%8.3f ms %4d  %s" % (v / 1e6, cnt[k], k))
+    # idle gaps: time between a kernel's end and the next kernel's start (host-bound stretches)
+    gaps = []
+    end = int(seg[0]["End_Timestamp"])
+    for prev, r in zip(seg, seg[1:]):
+        st = int(r["Start_Timestamp"])
+        if st > end:
+            gaps.append((st - end, prev["Kernel_Name"][:60], r["Kernel_Name"][:60]))
+        end = max(end, int(r["End_Timestamp"]))
+    gaps.sort(reverse=True)
+    print("idle total %.3f ms in %d gaps; largest:" % (sum(g[0] for g in gaps) / 1e6, len(gaps)))
+    for g in gaps[:12]:
+        print("  %7.3f ms  after %s  before %s" % (g[0] / 1e6, g[1], g[2]))
 
 
 if __name__ == "__main__":
