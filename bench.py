@@ -70,6 +70,10 @@ ARITHMETIC = {
 }
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E peak (spec)
 FLOP_PER_POINT_NS1 = 4761600 + 2101248   # NS*4,761,600 + 2,101,248
+# FLOP the fused kernel executes per point with the projected latent (lin_z folded into the
+# latent per scene): lin_in + 5 blocks x (fc_0 + fc_1) + lin_out
+KERNEL_FLOP_PER_POINT_NS1 = 2 * 42 * 512 + 5 * 2 * 2 * 512 * 512 + 2 * 512 * 4   # 5,289,984
+PROJ_FLOP_PER_SCENE = 2 * 3 * 64 * 64 * 512 * 512   # 3 lin_z layers x 4096 latent pixels
 KC, KF = 64, 64
 CHUNK = 4096
 W = H = 128
@@ -222,6 +226,7 @@ def _time_render(net, renderer, rays, chunk, passes=2):
     render_par = renderer.bind_parallel(net, simple_output=True).eval()
 
     def once():
+        net.drop_latent_proj()   # per-scene projection rebuilt in every timed pass
         for r in torch.split(rays, chunk, dim=0):
             render_par(r[None])
 
@@ -235,7 +240,7 @@ def _time_render(net, renderer, rays, chunk, passes=2):
     return (time.perf_counter() - t0) / passes
 
 
-def extra_configs(dev, precision):
+def extra_configs(dev, precision, latent_proj=True):
     """The other SURVEY §8(d) workloads on 1 GPU (informational, not `value`):
     cfg2 with the shipped conf (64 + 32 incl. 16 depth samples), cfg3 NMR 64x64 (latent
     32x32, 24 frames x 4096 rays), cfg4 DTU 400x300 with NS = 3 source views (one 120,000-
@@ -248,6 +253,7 @@ def extra_configs(dev, precision):
         net.load_state_dict(sd, strict=False)
         net = net.to(dev).eval()
         net.mlp_precision = precision
+        net.use_latent_proj = latent_proj
         net.encode_latent(latent.to(dev), poses.to(dev), focal.to(dev), size,
                           c=c.to(dev) if c is not None else None, num_objs=n_obj)
         return net
@@ -311,6 +317,8 @@ def main():
     ap.add_argument("--no-compare", action="store_true",
                     help="skip the f32-MFMA comparison frame (profiling runs)")
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
+    ap.add_argument("--no-latent-proj", action="store_true",
+                    help="per-point lin_z GEMMs on the gathered latent (A/B against the projection)")
     args = ap.parse_args()
 
     rank, world, local = pdist.init_from_env("nccl")   # RCCL on ROCm; control plane only
@@ -319,6 +327,7 @@ def main():
 
     sd, net, rays = build_scene(dev, rank)
     net.mlp_precision = args.precision
+    net.use_latent_proj = not args.no_latent_proj
     renderer = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True,
                             eval_batch_size=CHUNK).to(dev)
     render_par = renderer.bind_parallel(net, [local], simple_output=True).eval()
@@ -327,7 +336,7 @@ def main():
     ev = HipEvents()
 
     # instrument the fused render: record events around every kernel of each chunk
-    orig = lib.pnr_render_forward
+    orig = lib.pnr_render_forward_proj
     pool = []
     recording = {"on": False}
 
@@ -337,11 +346,14 @@ def main():
         evs = ev.create(7)
         pool.append(evs)
         arr = (ctypes.c_void_p * 7)(*[e.value for e in evs])
-        return lib.pnr_render_forward_events(*a, arr)
+        return orig(*a[:-1], arr)
 
-    lib.pnr_render_forward = render_with_events
+    lib.pnr_render_forward_proj = render_with_events
 
     def step():
+        # the per-scene latent projection (lin_z folded into the latent) is rebuilt inside
+        # every timed frame: nothing beyond the encoder latent is carried across steps
+        net.drop_latent_proj()
         frame = []
         for r in chunks:
             rgb, _depth = render_par(r[None])
@@ -376,8 +388,10 @@ def main():
             per[n].append(ev.elapsed_ms(evs[i], evs[i + 1]))
     avg = {n: sum(v) / len(v) for n, v in per.items()}
     pts_fine = CHUNK * (KC + KF)
-    flop_fine = pts_fine * FLOP_PER_POINT_NS1
+    kflop = KERNEL_FLOP_PER_POINT_NS1 if net.use_latent_proj else FLOP_PER_POINT_NS1
+    flop_fine = pts_fine * kflop
     achieved = flop_fine / (avg["mlp_fine"] * 1e-3) / 1e12
+    ref_equiv = pts_fine * FLOP_PER_POINT_NS1 / (avg["mlp_fine"] * 1e-3) / 1e12
     peak, terms = PEAK_BY_PRECISION[args.precision]
 
     # same frame with the plain f32-MFMA arithmetic, for comparison (N = 1 only)
@@ -395,7 +409,8 @@ def main():
         net.mlp_precision = args.precision
 
     prec_code = PRECISIONS[args.precision]
-    traffic, traffic_src = pmc_traffic("k_point_mlp<%d>" % prec_code, "fine")
+    kname = "k_point_mlp<%d, %s>" % (prec_code, "true" if net.use_latent_proj else "false")
+    traffic, traffic_src = pmc_traffic(kname, "fine")
     rays_total = W * H * args.steps * world
     value = rays_total / elapsed
     out = {
@@ -417,17 +432,24 @@ def main():
                                "(64 coarse + 64 fine)", "frame": [W, H], "chunk_rays": CHUNK,
                    "n_coarse": KC, "n_fine": KF, "n_views": 1, "rays_per_step_per_gpu": W * H,
                    "parallelism": "rays sharded by frame, 1 process per GPU"},
+        "latent_proj": {"on": bool(net.use_latent_proj),
+                        "flop_per_scene_per_mlp": PROJ_FLOP_PER_SCENE,
+                        "note": "lin_z of every latent pixel (pnr_latent_project), rebuilt for both "
+                                "MLPs inside every timed step; the kernel blends 4 projected rows per "
+                                "point instead of 3 per-point 512x512 lin_z GEMMs"},
         "roofline": {"kernel": "k_point_mlp (fine pass)", "bound": "mfma",
                      "achieved": round(achieved, 2), "peak": round(peak, 1),
-                     "unit": "TFLOP/s (fp32-equivalent: algorithmic FLOP / launch time)",
+                     "unit": "TFLOP/s (fp32-equivalent: the kernel's algorithmic FLOP per launch / "
+                             "launch time; %d FLOP per point)" % kflop,
+                     "reference_equivalent_tflops": round(ref_equiv, 2),
                      "frac": round(achieved / peak, 4),
                      "mfma_issue": {"tflops": round(achieved * terms, 1),
                                     "peak": MFMA_F32_PEAK_TFLOPS if terms == 1 else MFMA_BF16_PEAK_TFLOPS,
                                     "products_per_fma": terms},
                      "traffic": traffic,
                      "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
-                                       "bench, fine-pass launches of k_point_mlp<%d> (%s, FETCH x2 "
-                                       "gfx950 correction)" % (prec_code, traffic_src),
+                                       "bench, fine-pass launches of %s (%s, FETCH x2 "
+                                       "gfx950 correction)" % (kname, traffic_src),
                      "flop_per_launch": flop_fine,
                      "launch_ms": round(avg["mlp_fine"], 4)},
         "kernel_ms": {n: round(v, 4) for n, v in avg.items()},
@@ -435,7 +457,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_composite:
         out["composite"] = composite_roofline(dev, ev)
     if rank == 0 and world == 1 and not args.no_extra:
-        out["extra_configs"] = extra_configs(dev, args.precision)
+        out["extra_configs"] = extra_configs(dev, args.precision, not args.no_latent_proj)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"], ref, streams = cpu_baseline(sd, rays.cpu(), args.cpu_rays)
         out["psnr_vs_reference_path"] = psnr_vs_reference_path(net, rays[:args.cpu_rays], ref, streams, dev)

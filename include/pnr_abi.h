@@ -179,6 +179,37 @@ int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
                               void *workspace, size_t workspace_bytes, pnr_stream_t stream,
                               void *const *events);
 
+/* ---- projected latent (lin_z folded into the latent, inference) --------------- */
+/* Floats-as-bytes of one model's projected latent for `scene`: n_linz x (n_obj * n_views)
+ * x latent_h x latent_w x 512 fp32, n_linz = min(combine_layer, n_blocks); 0 if invalid. */
+size_t pnr_latent_project_bytes(const pnr_scene *scene, const pnr_mlp_desc *desc);
+
+/* Replaces: the per-point lin_z GEMMs of ResnetFC (resnetfc.py:160-163) on the bilinearly
+ * sampled latent (encoder.py:102-108).  grid_sample's output is a blend of four latent
+ * pixels and lin_z is linear, so lin_z[b](z) = blend of the rows of
+ *   proj[b][image][y][x][:] = lin_z[b].weight . latent[image][y][x][:]      (no bias)
+ * computed here once per (scene, weight version) with fp32 products and accumulation.
+ * The *_proj entry points below blend four rows per point instead of the lin_z GEMM
+ * (same results up to fp32 reassociation).  Forward (inference) only. */
+int pnr_latent_project(const pnr_scene *scene, const pnr_mlp_weights *w, float *proj, size_t proj_bytes,
+                       pnr_stream_t stream);
+
+/* pnr_point_query / pnr_render_forward_events with the projected latent of the model(s):
+ * `proj` (point query), `coarse_proj` / `fine_proj` (render; pass the coarse projection
+ * twice when mlp_fine is None) from pnr_latent_project on the same scene and weights.
+ * NULL projections select the latent gather + lin_z GEMM path.  `events` may be NULL. */
+int pnr_point_query_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                         const float *proj, const float *xyz, const float *viewdirs,
+                         int64_t points_per_obj, float *out, void *workspace,
+                         size_t workspace_bytes, pnr_stream_t stream);
+int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc,
+                            const void *coarse_packed, const void *fine_packed,
+                            const float *coarse_proj, const float *fine_proj,
+                            const pnr_rays *rays, const pnr_rng *rng,
+                            const pnr_render_cfg *cfg, const pnr_render_out *out,
+                            void *workspace, size_t workspace_bytes, pnr_stream_t stream,
+                            void *const *events);
+
 /* ---- building blocks (also the generic model-callback path) ------------------ */
 /* Replaces: NeRFRenderer.sample_coarse (nerf.py:98-118).  z (n_rays, n_coarse). */
 int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse,

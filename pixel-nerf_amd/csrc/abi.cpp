@@ -40,7 +40,9 @@ int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, co
                          float *, hipStream_t);
 int launch_point_mlp(const pnr_scene &, const pnr_mlp_desc &, const void *, const float *,
                      const float *, int, int64_t, const float *, const float *, int64_t, int64_t,
-                     float *, float *, hipStream_t, float *save = nullptr);
+                     float *, float *, hipStream_t, float *save = nullptr, const float *proj = nullptr);
+int64_t latent_proj_floats(const pnr_scene &, const pnr_mlp_desc &);
+int launch_latent_proj(const pnr_scene &, const pnr_mlp_weights &, float *, size_t, hipStream_t);
 
 static thread_local char g_err[1024];
 
@@ -126,6 +128,29 @@ size_t pnr_point_query_workspace_bytes(const pnr_scene *scene, int64_t n_points)
 int pnr_point_query(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
                     const float *xyz, const float *viewdirs, int64_t points_per_obj, float *out,
                     void *workspace, size_t workspace_bytes, pnr_stream_t stream) {
+    return pnr_point_query_proj(scene, desc, packed, nullptr, xyz, viewdirs, points_per_obj, out, workspace,
+                                workspace_bytes, stream);
+}
+
+size_t pnr_latent_project_bytes(const pnr_scene *scene, const pnr_mlp_desc *desc) {
+    if (!scene || !desc || check_scene(scene) != PNR_OK || mlp_check_desc(*desc) != PNR_OK) return 0;
+    return sizeof(float) * (size_t)latent_proj_floats(*scene, *desc);
+}
+
+int pnr_latent_project(const pnr_scene *scene, const pnr_mlp_weights *w, float *proj, size_t proj_bytes,
+                       pnr_stream_t stream) {
+    int rc = check_scene(scene);
+    if (rc) return rc;
+    if (!w || !proj) return fail(PNR_ERR_INVALID, "pnr_latent_project: NULL argument");
+    if ((rc = check_desc_for_scene(&w->desc, scene))) return rc;
+    if ((reinterpret_cast<uintptr_t>(proj) & 15) != 0)
+        return fail(PNR_ERR_INVALID, "pnr_latent_project: proj must be 16-byte aligned");
+    return launch_latent_proj(*scene, *w, proj, proj_bytes, (hipStream_t)stream);
+}
+
+int pnr_point_query_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                         const float *proj, const float *xyz, const float *viewdirs, int64_t points_per_obj,
+                         float *out, void *workspace, size_t workspace_bytes, pnr_stream_t stream) {
     int rc = check_scene(scene);
     if (rc) return rc;
     if ((rc = check_desc_for_scene(desc, scene))) return rc;
@@ -136,9 +161,11 @@ int pnr_point_query(const pnr_scene *scene, const pnr_mlp_desc *desc, const void
     const size_t need = pnr_point_query_workspace_bytes(scene, n_points);
     if (need && (!workspace || workspace_bytes < need))
         return fail(PNR_ERR_WORKSPACE, "pnr_point_query: workspace %zu < %zu", workspace_bytes, need);
+    if (proj && (reinterpret_cast<uintptr_t>(proj) & 15) != 0)
+        return fail(PNR_ERR_INVALID, "pnr_point_query_proj: proj must be 16-byte aligned");
     return launch_point_mlp(*scene, *desc, packed, nullptr, nullptr, 0, 1, xyz, viewdirs,
                             points_per_obj, n_points, out, static_cast<float *>(workspace),
-                            (hipStream_t)stream);
+                            (hipStream_t)stream, nullptr, proj);
 }
 
 size_t pnr_point_save_floats(const pnr_mlp_desc *desc, int64_t n_points) {
@@ -273,6 +300,15 @@ int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
                               const pnr_rays *rays, const pnr_rng *rng, const pnr_render_cfg *cfg,
                               const pnr_render_out *out, void *workspace, size_t workspace_bytes,
                               pnr_stream_t stream, void *const *events) {
+    return pnr_render_forward_proj(scene, desc, coarse_packed, fine_packed, nullptr, nullptr, rays, rng, cfg,
+                                   out, workspace, workspace_bytes, stream, events);
+}
+
+int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *coarse_packed,
+                            const void *fine_packed, const float *coarse_proj, const float *fine_proj,
+                            const pnr_rays *rays, const pnr_rng *rng, const pnr_render_cfg *cfg,
+                            const pnr_render_out *out, void *workspace, size_t workspace_bytes,
+                            pnr_stream_t stream, void *const *events) {
     int rc = check_scene(scene);
     if (rc) return rc;
     if ((rc = check_desc_for_scene(desc, scene))) return rc;
@@ -283,6 +319,8 @@ int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
     if (kf < 0 || kfd < 0 || kfd > kf) return fail(PNR_ERR_INVALID, "need 0 <= n_fine_depth <= n_fine");
     if (kc + kf > 1024) return fail(PNR_ERR_UNSUPPORTED, "n_coarse + n_fine must be <= 1024");
     if (kf > 0 && !fine_packed) return fail(PNR_ERR_INVALID, "fine_packed is NULL");
+    if (((reinterpret_cast<uintptr_t>(coarse_proj) | reinterpret_cast<uintptr_t>(fine_proj)) & 15) != 0)
+        return fail(PNR_ERR_INVALID, "latent projections must be 16-byte aligned");
     const int64_t n = rays->n_rays;
     if (n < 0 || !rays->rays) return fail(PNR_ERR_INVALID, "bad rays");
     if (n == 0) return PNR_OK;
@@ -314,7 +352,7 @@ int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
     if ((rc = launch_sample_coarse(rays->rays, n, kc, rng->u_coarse, cfg->lindisp, zc, st))) return rc;
     if ((rc = mark(1))) return rc;
     if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj,
-                               nullptr, nullptr, 1, n * kc, rawc, xsum, st)))
+                               nullptr, nullptr, 1, n * kc, rawc, xsum, st, nullptr, coarse_proj)))
         return rc;
     if ((rc = mark(2))) return rc;
     if ((rc = launch_composite(zc, rawc, rays->rays, n, kc, cfg->white_bkgd, wc, out->coarse_rgb,
@@ -331,7 +369,7 @@ int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
         return rc;
     if ((rc = mark(4))) return rc;
     if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, zf, kall, rays->rays_per_obj,
-                               nullptr, nullptr, 1, n * kall, rawf, xsum, st)))
+                               nullptr, nullptr, 1, n * kall, rawf, xsum, st, nullptr, fine_proj)))
         return rc;
     if ((rc = mark(5))) return rc;
     if ((rc = launch_composite(zf, rawf, rays->rays, n, kall, cfg->white_bkgd, out->fine_weights,

@@ -314,6 +314,10 @@ struct Args {
     //   features (64) | z (512) | relu(x) into fc_0 of block b (512 each) |
     //   relu(h) of block b (512 each) | relu(x) into lin_out (512)          (save_floats())
     float *save;
+    // projected latent (k_latent_proj, PZ kernels): lin_z block b reads proj + b * proj_stride,
+    // (n_obj * n_views, H_l, W_l, 512) like the latent
+    const float *proj;
+    int64_t proj_stride;
 };
 
 // floats of the activation save per point (Args::save): the fp32 regions, then the relu
@@ -777,6 +781,57 @@ struct GemmCtx {
 #endif
 };
 
+// lin_z(z) - bias of the bilinear latent sample z of every column of the tile, staged in
+// LDS as fp32 stage[column][LDS_LD]: resnetfc.py:160-163 on grid_sample's blend
+// (encoder.py:102-108), evaluated by linearity as the blend of four rows of the projected
+// latent P = latent W_z^T (proj.hip), torch's nw, ne, sw, se summation order.  Wave w blends
+// the COLS / WAVES columns [8w, 8w + 8); each load instruction reads one contiguous 1 KB half
+// of a corner's 2 KB row.  Callers barrier before (the stage aliases the GEMM input image)
+// and after.
+__device__ __forceinline__ void stage_proj(float *stage, const float *__restrict__ pz, const float *gtab, int wave,
+                                           int lane) {
+#pragma unroll 4
+    for (int j = 0; j < COLS / WAVES; ++j) {
+        const int cj = (COLS / WAVES) * wave + j;
+        const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
+        const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const uint32_t ch = half * 256 + lane * 4;
+#ifdef PNR_ABLATE_GATHER
+            const f4 c0 = tw, c1 = to, c2 = tw, c3 = to;   // diagnostic: no loads
+#else
+            const f4 c0 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.x) + ch);
+            const f4 c1 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.y) + ch);
+            const f4 c2 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.z) + ch);
+            const f4 c3 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.w) + ch);
+#endif
+            f4 zz;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                zz[q] = add_rn(add_rn(add_rn(mul_rn(c0[q], tw.x), mul_rn(c1[q], tw.y)), mul_rn(c2[q], tw.z)),
+                               mul_rn(c3[q], tw.w));
+            *reinterpret_cast<f4 *>(stage + cj * LDS_LD + ch) = zz;
+        }
+    }
+}
+static_assert(sizeof(float) * COLS * LDS_LD <= 2 * sizeof(_Float16) * PART_HALVES,
+              "the fp32 stage fits in the split image it aliases");
+// x[r][c] += stage rows of this wave (column 16c + cl, rows 16 (RTW wave + r) + 4g ..)
+__device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, int lane) {
+    const int g = lane >> 4, cl = lane & 15;
+#pragma unroll
+    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+            const f4 v = *reinterpret_cast<const f4 *>(stage + (16 * c + cl) * LDS_LD + 16 * (RTW * wave + r) + 4 * g);
+            f4 o;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = add_rn(x[r][c][q], v[q]);
+            x[r][c] = o;
+        }
+}
+
 // hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index)
 template <int PREC, int NK>
 __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx) {
@@ -811,7 +866,8 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
     PT(g, 2);
 }
 
-template <int PREC>
+// PZ: lin_z from the projected latent (gather_proj) instead of the latent gather + GEMM
+template <int PREC, bool PZ>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
@@ -1018,6 +1074,17 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
+                if constexpr (PZ) {
+                    // the stage aliases the image the previous GEMM read; publish_relu's
+                    // internal barrier orders the add_stage reads before the image writes
+                    __syncthreads();
+                    PT(gc, 3);
+                    stage_proj(inbuf, a.proj + blk * a.proj_stride, gtab, wave, lane);
+                    __syncthreads();
+                    PT(gc, 1);
+                    add_bias(x, bias + (1 + lz) * H, wave, g, true);
+                    add_stage(x, inbuf, wave, lane);
+                } else {
                 __syncthreads();
                 PT(gc, 3);
                 // z = bilinear latent gather (torch's nw, ne, sw, se summation order).
@@ -1073,6 +1140,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 __syncthreads();
+                }
                 publish_relu(x, tile, blk);
                 if constexpr (PREC != 0 && kParkX) park(x, xp);
                 __syncthreads();
@@ -1538,8 +1606,10 @@ size_t mlp_xsum_bytes(int ns) {
 int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *packed,
                      const float *rays, const float *zs, int K, int64_t rays_per_obj,
                      const float *xyz, const float *dirs, int64_t points_per_obj,
-                     int64_t n_points, float *out, float *xsum_ws, hipStream_t st, float *save) {
+                     int64_t n_points, float *out, float *xsum_ws, hipStream_t st, float *save,
+                     const float *proj) {
     if (n_points == 0) return PNR_OK;
+    if (proj && save) return fail(PNR_ERR_UNSUPPORTED, "the activation save (training) needs the latent gather path");
     mlpk::Args a = {};
     a.packed = static_cast<const float *>(packed);
     a.L = mlpk::make_layout(d);
@@ -1554,6 +1624,8 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.xsum = xsum_ws;
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
     a.save = save;
+    a.proj = proj;
+    a.proj_stride = (int64_t)sc.n_obj * sc.n_views * sc.latent_h * sc.latent_w * mlpk::H;
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
     // PREC 3: split image P0 + P1, gather records, column maxima, exponents = 139,520 B
@@ -1561,19 +1633,18 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     const size_t lds = d.precision == PNR_PREC_F16X3
         ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS)
         : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8);
+#define PNR_LAUNCH_MLP(P)                                                                              \
+    do {                                                                                               \
+        if (proj) hipLaunchKernelGGL((mlpk::k_point_mlp<P, true>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \
+        else hipLaunchKernelGGL((mlpk::k_point_mlp<P, false>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);     \
+    } while (0)
     switch (d.precision) {
-    case PNR_PREC_F16X3:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<3>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
-        break;
-    case PNR_PREC_BF16X6:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<6>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
-        break;
-    case PNR_PREC_BF16X9:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<9>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
-        break;
-    default:
-        hipLaunchKernelGGL(mlpk::k_point_mlp<0>, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
+    case PNR_PREC_F16X3: PNR_LAUNCH_MLP(3); break;
+    case PNR_PREC_BF16X6: PNR_LAUNCH_MLP(6); break;
+    case PNR_PREC_BF16X9: PNR_LAUNCH_MLP(9); break;
+    default: PNR_LAUNCH_MLP(0);
     }
+#undef PNR_LAUNCH_MLP
     return launch_ok("point_mlp") ? PNR_OK : PNR_ERR_HIP;
 }
 

@@ -79,6 +79,14 @@ SIGNATURES = {
                                           ctypes.POINTER(Rays), ctypes.POINTER(Rng),
                                           ctypes.POINTER(RenderCfg), ctypes.POINTER(RenderOut),
                                           c_vp, c_size, c_vp, ctypes.POINTER(c_vp)]),
+    "pnr_latent_project_bytes": (c_size, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc)]),
+    "pnr_latent_project": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpWeights), c_vp, c_size, c_vp]),
+    "pnr_point_query_proj": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp, c_vp, c_vp, c_vp,
+                                     c_i64, c_vp, c_vp, c_size, c_vp]),
+    "pnr_render_forward_proj": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp, c_vp, c_vp, c_vp,
+                                        ctypes.POINTER(Rays), ctypes.POINTER(Rng),
+                                        ctypes.POINTER(RenderCfg), ctypes.POINTER(RenderOut),
+                                        c_vp, c_size, c_vp, ctypes.POINTER(c_vp)]),
     "pnr_sample_coarse": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "pnr_sample_fine": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f, c_vp,
                                 c_vp, c_vp, c_i32, c_vp, c_vp]),

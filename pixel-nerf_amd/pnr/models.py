@@ -11,6 +11,7 @@ device; the nn.Linear modules here are the parameter store the kernels read
 import os
 import os.path as osp
 import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -209,6 +210,34 @@ class ResnetFC(nn.Module):
         self.__dict__["_pnr_pack_t"] = (key, buf_t, keep)
         return desc, buf, buf_t
 
+    def latent_proj(self, code, scene, latent):
+        """Projected latent of this MLP's lin_z layers for the encoded scene
+        (pnr_latent_project: lin_z[b].weight . latent at every latent pixel, fp32), which the
+        fused kernel blends per point instead of running the lin_z GEMMs (resnetfc.py:160-163;
+        exact by linearity of grid_sample's bilinear blend).  Cached per (weight version,
+        latent tensor + version); None if the MLP has no lin_z layers."""
+        if len(getattr(self, "lin_z", [])) == 0:
+            return None
+        key = self._pack_key(code, None)
+        cache = self.__dict__.get("_pnr_proj")
+        if (cache is not None and cache[0] == key and cache[1]() is latent
+                and cache[2] == latent._version):
+            return cache[3]
+        desc = self.desc(int(code._freqs.numel()))
+        lib = _lib.load()
+        nbytes = lib.pnr_latent_project_bytes(scene, desc)
+        if nbytes == 0:
+            _lib.check(-1, "pnr_latent_project_bytes")
+        buf = torch.empty(nbytes // 4, dtype=torch.float32, device=latent.device)
+        w, keep = self._weights(code, desc)
+        _lib.check(lib.pnr_latent_project(scene, w, _lib.ptr(buf), nbytes, _lib.stream_of(latent.device)),
+                   "pnr_latent_project")
+        self.__dict__["_pnr_proj"] = (key, weakref.ref(latent), latent._version, buf, keep)
+        return buf
+
+    def drop_latent_proj(self):
+        self.__dict__.pop("_pnr_proj", None)
+
 
 def make_mlp(conf, d_in, d_latent=0, allow_empty=False, **kwargs):
     """model_util.py:5-15 (type = resnet is the implemented MLP)."""
@@ -271,6 +300,9 @@ class PixelNeRFNet(nn.Module):
         # GEMM arithmetic of the fused kernel (see PRECISIONS): the scaled split-fp16 mode
         # has fp32-level error at 3.2x the f32-MFMA throughput
         self.mlp_precision = "f16x3"
+        # inference: fold lin_z into the latent once per (scene, weights) and blend four
+        # projected rows per point (ResnetFC.latent_proj) instead of the per-point lin_z GEMMs
+        self.use_latent_proj = True
 
     # ---- encode ---------------------------------------------------------------------
     def encode(self, images, poses, focal, z_bounds=None, c=None):
@@ -399,6 +431,21 @@ class PixelNeRFNet(nn.Module):
             raise ValueError("mlp_precision must be one of %s" % sorted(PRECISIONS))
         return mlp.packed(self.code, self.mlp_precision)
 
+    def hip_proj(self, coarse, scene=None):
+        """Device pointer-holder of the projected latent for the coarse / fine MLP, or None
+        (use_latent_proj off, or no lin_z layers)."""
+        if not self.use_latent_proj:
+            return None
+        mlp = self.mlp_coarse if (coarse or self.mlp_fine is None) else self.mlp_fine
+        return mlp.latent_proj(self.code, scene if scene is not None else self.hip_scene(),
+                               self.encoder.latent_cl)
+
+    def drop_latent_proj(self):
+        """Forget the cached projections (they are rebuilt on the next render)."""
+        for mlp in (self.mlp_coarse, self.mlp_fine):
+            if mlp is not None:
+                mlp.drop_latent_proj()
+
     # ---- forward (point query) -----------------------------------------------------
     def forward(self, xyz, coarse=True, viewdirs=None, far=False):
         """(SB, B, 3) world points -> (SB, B, 4) [sigmoid(rgb), relu(sigma)]
@@ -413,13 +460,14 @@ class PixelNeRFNet(nn.Module):
         vd = _dev(viewdirs.reshape(SB, B, 3), "viewdirs") if viewdirs is not None else None
         desc, packed = self.hip_mlp(coarse)
         sc = self.hip_scene()
+        proj = self.hip_proj(coarse, sc)
         lib = _lib.load()
         ws_bytes = lib.pnr_point_query_workspace_bytes(sc, SB * B)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xyz.device)
         out = torch.empty(SB, B, 4, dtype=torch.float32, device=xyz.device)
-        _lib.check(lib.pnr_point_query(sc, desc, _lib.ptr(packed), _lib.ptr(xyz), _lib.ptr(vd), B,
-                                       _lib.ptr(out), _lib.ptr(ws), ws_bytes,
-                                       _lib.stream_of(xyz.device)), "pnr_point_query")
+        _lib.check(lib.pnr_point_query_proj(sc, desc, _lib.ptr(packed), _lib.ptr(proj), _lib.ptr(xyz),
+                                            _lib.ptr(vd), B, _lib.ptr(out), _lib.ptr(ws), ws_bytes,
+                                            _lib.stream_of(xyz.device)), "pnr_point_query_proj")
         return out
 
     # ---- checkpoints (models.py:268-316) -------------------------------------------

@@ -234,6 +234,8 @@ class NeRFRenderer(torch.nn.Module):
         sc = net.hip_scene()
         desc, pc = net.hip_mlp(True)
         _, pf = net.hip_mlp(False) if kf > 0 else (None, None)
+        zc = net.hip_proj(True, sc)
+        zf = net.hip_proj(False, sc) if kf > 0 else None
         f32 = dict(device=dev, dtype=torch.float32)
         c_rgb, c_depth = torch.empty(B, 3, **f32), torch.empty(B, **f32)
         c_w = torch.empty(B, kc, **f32) if want_weights or kf > 0 else None
@@ -252,9 +254,9 @@ class NeRFRenderer(torch.nn.Module):
         lib = _lib.load()
         ws_bytes = lib.pnr_render_workspace_bytes(sc, cfg, B)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        _lib.check(lib.pnr_render_forward(sc, desc, _lib.ptr(pc), _lib.ptr(pf) if pf is not None else None,
-                                          r, rng, cfg, out, _lib.ptr(ws), ws_bytes,
-                                          _lib.stream_of(dev)), "pnr_render_forward")
+        _lib.check(lib.pnr_render_forward_proj(sc, desc, _lib.ptr(pc), _lib.ptr(pf), _lib.ptr(zc), _lib.ptr(zf),
+                                               r, rng, cfg, out, _lib.ptr(ws), ws_bytes,
+                                               _lib.stream_of(dev), None), "pnr_render_forward_proj")
         outputs = DotMap(coarse=self._pack_out(c_w, c_rgb, c_depth, sb, want_weights))
         if kf > 0:
             outputs.fine = self._pack_out(f_w, f_rgb, f_depth, sb, want_weights)

@@ -14,6 +14,7 @@ n = int(os.environ.get("N_CHUNKS", "2"))
 dev = torch.device("cuda:0")
 sd, net, rays = bench.build_scene(dev, 0)
 net.mlp_precision = prec
+net.use_latent_proj = os.environ.get("LATENT_PROJ", "1") == "1"
 r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True)
 import time  # noqa: E402
 
@@ -31,7 +32,7 @@ with torch.no_grad():
     for i in range(n):
         r(net, rays[:4096][None])
     torch.cuda.synchronize()
-print("done", prec, n, "chunk_ms %.3f" % ((time.perf_counter() - t0) / n * 1e3),
+print("done", prec, "proj" if net.use_latent_proj else "gather", n, "chunk_ms %.3f" % ((time.perf_counter() - t0) / n * 1e3),
       os.environ.get("PNR_LIB_PATH", "default"))
 if dbg is not None:
     dbg(ph, 0)

@@ -53,9 +53,10 @@ def model_conf(n_blocks=5, combine_layer=3):
 PRECS = ["fp32", "f16x3", "bf16x6", "bf16x9"]
 
 
-def hip_net(cfg, arr, precision="f16x3"):
+def hip_net(cfg, arr, precision="f16x3", latent_proj=True):
     net = PixelNeRFNet(model_conf(cfg.get("n_blocks", 5), cfg.get("combine_layer", 3)))
     net.mlp_precision = precision
+    net.use_latent_proj = latent_proj
     if not cfg.get("with_fine", True):
         net.mlp_fine = None      # as eval_approx.py:62-63 does
     sd = fixtures.state_dict(cfg)
@@ -70,8 +71,8 @@ def hip_net(cfg, arr, precision="f16x3"):
     return net
 
 
-def hip_render(cfg, arr, want_weights=True, precision="f16x3"):
-    net = hip_net(cfg, arr, precision)
+def hip_render(cfg, arr, want_weights=True, precision="f16x3", latent_proj=True):
+    net = hip_net(cfg, arr, precision, latent_proj)
     r = NeRFRenderer(n_coarse=cfg["n_coarse"], n_fine=cfg["n_fine"], n_fine_depth=cfg["n_fine_depth"],
                      depth_std=cfg["depth_std"], white_bkgd=cfg["white_bkgd"], lindisp=cfg["lindisp"])
     r.streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
@@ -160,11 +161,44 @@ def test_sample_fine_matches_oracle(kc, kf, kfd, lindisp):
 
 
 # ------------------------------------------------------------------- model --
+def test_latent_project_matches_fp64():
+    """pnr_latent_project: lin_z[b].weight . latent at every latent pixel (no bias), the
+    per-scene table the kernel blends instead of the per-point lin_z GEMMs, vs fp64; SB=2
+    objects x NS=3 views, a pixel count that is not a multiple of the 64-row tile."""
+    sd = synth.pixelnerf_state(4)
+    sb, ns = 2, 3
+    lat = synth.latent(9, sb * ns, 512, 7, 9)
+    net = PixelNeRFNet(model_conf())
+    net.load_state_dict(sd, strict=False)
+    net = net.to(DEV).eval()
+    poses = synth.srn_poses([10.0 * i for i in range(sb * ns)]).reshape(sb, ns, 4, 4)
+    net.encode_latent(lat.to(DEV), poses.to(DEV), torch.tensor(50.0, device=DEV), (64, 64), num_objs=sb)
+    for mlp, pre in ((net.mlp_coarse, "mlp_coarse"), (net.mlp_fine, "mlp_fine")):
+        proj = mlp.latent_proj(net.code, net.hip_scene(), net.encoder.latent_cl).cpu().reshape(3, -1, 512)
+        lat_cl = lat.permute(0, 2, 3, 1).reshape(-1, 512).double()
+        for b in range(3):
+            w = sd["%s.lin_z.%d.weight" % (pre, b)].double()
+            ref = lat_cl @ w.t()
+            scale = float((lat_cl.abs() @ w.abs().t()).max())
+            err = float((proj[b].double() - ref).abs().max())
+            assert err <= 2e-6 * scale, (pre, b, err, scale)
+    # cached per (weights, latent); a new latent or a weight update rebuilds it
+    p1 = net.mlp_coarse.latent_proj(net.code, net.hip_scene(), net.encoder.latent_cl)
+    assert p1 is net.mlp_coarse.latent_proj(net.code, net.hip_scene(), net.encoder.latent_cl)
+    with torch.no_grad():
+        net.mlp_coarse.lin_z[0].weight.mul_(2.0)
+    p2 = net.mlp_coarse.latent_proj(net.code, net.hip_scene(), net.encoder.latent_cl)
+    assert p2 is not p1
+    torch.testing.assert_close(p2.reshape(3, -1, 512)[0].cpu(), 2.0 * p1.reshape(3, -1, 512)[0].cpu(),
+                               rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("latent_proj", [True, False])
 @pytest.mark.parametrize("precision", PRECS)
-def test_point_query_matches_reference_fixture(precision):
+def test_point_query_matches_reference_fixture(precision, latent_proj):
     cfg, arr = fixtures.load("fw_pointquery")
     net = hip_net(dict(cfg, n_blocks=5, combine_layer=3, with_fine=True, d_latent=512,
-                       d_hidden=512), arr, precision)
+                       d_hidden=512), arr, precision, latent_proj)
     with torch.no_grad():
         vd = torch.zeros_like(arr["xyz"]).to(DEV)
         oc = net(arr["xyz"].to(DEV), coarse=True, viewdirs=vd)
@@ -173,8 +207,9 @@ def test_point_query_matches_reference_fixture(precision):
     assert_close(of, arr["out_fine"], "point query fine")
 
 
+@pytest.mark.parametrize("latent_proj", [True, False])
 @pytest.mark.parametrize("precision", PRECS)
-def test_point_query_multiview_multiobject_vs_oracle(precision):
+def test_point_query_multiview_multiobject_vs_oracle(precision, latent_proj):
     """SB=2 objects x NS=3 views, per-object focal/c; checks the x_sum combine path."""
     torch.manual_seed(0)
     sb, ns, P = 2, 3, 200
@@ -190,6 +225,7 @@ def test_point_query_multiview_multiobject_vs_oracle(precision):
         ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, True, vd)
     net = PixelNeRFNet(model_conf())
     net.mlp_precision = precision
+    net.use_latent_proj = latent_proj
     net.load_state_dict(sd, strict=False)
     net = net.to(DEV).eval()
     net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (64, 60), c=c.to(DEV), num_objs=sb)
@@ -198,9 +234,10 @@ def test_point_query_multiview_multiobject_vs_oracle(precision):
     assert_close(out, ref, "point query SB=2 NS=3")
 
 
+@pytest.mark.parametrize("latent_proj", [True, False])
 @pytest.mark.parametrize("precision", ["fp32", "f16x3"])
 @pytest.mark.parametrize("lat_scale,w_scale", [(1e-4, 1.0), (1e3, 1.0), (1.0, 1e-3), (0.0, 1.0)])
-def test_point_query_dynamic_range(precision, lat_scale, w_scale):
+def test_point_query_dynamic_range(precision, lat_scale, w_scale, latent_proj):
     """Scaled-fp16 mode keeps fp32-level error when the latent / lin_z weights are far
     from unit scale (per-column and per-layer power-of-two scaling), and on all-zero
     latent columns.  Tolerance relative to the output's magnitude."""
@@ -218,6 +255,7 @@ def test_point_query_dynamic_range(precision, lat_scale, w_scale):
         ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, True, vd)
     net = PixelNeRFNet(model_conf())
     net.mlp_precision = precision
+    net.use_latent_proj = latent_proj
     net.load_state_dict(sd, strict=False)
     net = net.to(DEV).eval()
     net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (64, 64))
@@ -285,6 +323,16 @@ def test_render_matches_reference_fixture(name, precision):
     out = hip_render(cfg, arr, precision=precision)
     frac = compare_render(name, out, cfg, arr)
     print("%s/%s: fine-bin flip fraction %.4f" % (name, precision, frac))
+
+
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
+@pytest.mark.parametrize("name", ["fw_cfg2", "fw_shipped", "fw_dtu_ns3"])
+def test_render_gather_path_matches_reference_fixture(name, precision):
+    """The per-point lin_z GEMM path (use_latent_proj = False: latent gather + lin_z on the
+    MFMA chain, the training forward's arithmetic) against the same fixtures."""
+    cfg, arr = fixtures.load(name)
+    out = hip_render(cfg, arr, precision=precision, latent_proj=False)
+    compare_render(name + "/gather", out, cfg, arr)
 
 
 def test_render_multiobject_vs_oracle():
