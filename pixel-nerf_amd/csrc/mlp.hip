@@ -712,7 +712,11 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
                                          bool accumulate) {
 #pragma unroll
     for (int r = 0; r < RTW; ++r) {
+#ifdef PNR_ABLATE_BIAS
+        const f4 b = f4{0.01f, 0.02f, 0.03f, 0.04f} * (float)(r + 1);   // diagnostic: no bias loads
+#else
         const f4 b = *reinterpret_cast<const f4 *>(bias + 16 * (RTW * wave + r) + 4 * g);
+#endif
 #pragma unroll
         for (int c = 0; c < CT; ++c) acc[r][c] = accumulate ? acc[r][c] + b : b;
     }
@@ -754,7 +758,8 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
 // cycles per phase, summed over workgroups: 0 features/projection, 1 latent gather,
 // 2 GEMMs, 3 glue (bias, relu stores, barriers), 4 lin_out head, 5 GEMM calls, 6 tiles.
 #ifdef PNR_PHASE_TIMING
-__device__ unsigned long long g_phase[8];
+constexpr int PT_SLOTS = 16;
+__device__ unsigned long long g_phase[PT_SLOTS];
 #define PT(gc, i)                                                     \
     do {                                                              \
         const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
@@ -762,7 +767,9 @@ __device__ unsigned long long g_phase[8];
         (gc).pt_last = t_;                                            \
     } while (0)
 #define PT_COUNT(gc, i) ((gc).pt[i] += 1)
+#define PT_WAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 #else
+#define PT_WAIT() ((void)0)
 #define PT(gc, i) ((void)0)
 #define PT_COUNT(gc, i) ((void)0)
 #endif
@@ -777,7 +784,7 @@ struct GemmCtx {
     const int *ecol;          // PREC 3: scale exponent of each IN column
     int wave, lane;
 #ifdef PNR_PHASE_TIMING
-    uint64_t pt[8], pt_last;
+    uint64_t pt[PT_SLOTS], pt_last;
 #endif
 };
 
@@ -878,8 +885,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     const int cl = lane & 15;
     const Layout &L = a.L;
     const float *bias = a.packed + L.off_bias;
-    const float *pe_f = a.packed;        // code._freqs  (pack header)
-    const float *pe_p = a.packed + 16;   // code._phases
 
     // per-lane fragment bases
     const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;         // f32 fragments
@@ -897,6 +902,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     float *gtab = PREC == 3 ? reinterpret_cast<float *>(P1 + PART_HALVES) : gc.stg + 2 * STG_FLOATS;
     float *cmax = gtab + COLS * 8;           // PREC 3: per-column partial maxima (64 x 8)
     int *ecol = reinterpret_cast<int *>(cmax + COLS * 8);
+    // PE freqs [0, 16) / phases [16, 32) of the pack header, in LDS: the feature loop indexes
+    // them per lane, and vector global loads there put a memory latency in every iteration
+    float *petab = PREC == 3 ? reinterpret_cast<float *>(ecol + COLS) : gtab + COLS * 8;
+    if (tid < 32) petab[tid] = a.packed[tid];   // visible after the first barrier of a tile
     gc.hdr = a.packed;
     // B fragment (column 16c + cl, k 32 ks + 8g): swz keeps it linear in ks and c
     gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
@@ -905,7 +914,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.wave = wave;
     gc.lane = lane;
 #ifdef PNR_PHASE_TIMING
-    for (int i = 0; i < 8; ++i) gc.pt[i] = 0;
+    for (int i = 0; i < PT_SLOTS; ++i) gc.pt[i] = 0;
     gc.pt_last = __builtin_amdgcn_s_memtime();
 #endif
     // feature role: thread -> (column col, part qt of WAVES); FPT features each
@@ -918,6 +927,16 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     float *sv_f = a.save, *sv_z = a.save ? a.save + P * 64 : nullptr;
     auto sv_slot = [&](int i) { return sv_z + P * H * (1 + i); };   // i: block b -> x_in, nb + b -> h, 2nb -> x_f
     uint32_t *sv_mask = a.save ? reinterpret_cast<uint32_t *>(a.save + save_mask_offset(L.n_blocks, P)) : nullptr;
+    // Barrier between a GEMM that reads the input image and the publish that rewrites it.
+    // PREC 3's publish writes only its column maxima before its own internal barrier, and
+    // the image after it, so there the barrier is redundant and waves that finish their GEMM
+    // early start the publish VALU under their SIMD-mate's MFMAs.
+    auto pre_publish_sync = [&]() {
+#ifndef PNR_GEMM_ONLY
+        if constexpr (PREC != 3)
+#endif
+            __syncthreads();
+    };
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx) {
         if (a.save) {
             save_relu(acc, sv_slot(save_idx), tile, P, wave, lane);
@@ -950,7 +969,20 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     __syncthreads();
 #endif
     Acc x, h;
-    for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+    // XCD-aware tile order: workgroups are placed round-robin on the 8 XCDs (blockIdx.x % 8),
+    // so XCD x walks the contiguous tile range [x T / 8, (x + 1) T / 8).  Neighbouring tiles
+    // are neighbouring rays, which sample neighbouring latent pixels: each XCD's L2 then holds
+    // its own band of the (projected) latent instead of all of it.
+    int64_t t_begin = blockIdx.x, t_end = a.n_tiles, t_step = gridDim.x;
+#ifndef PNR_PLAIN_TILE_ORDER
+    if (gridDim.x % 8 == 0) {
+        const int64_t xcd = blockIdx.x % 8;
+        t_begin = xcd * a.n_tiles / 8 + blockIdx.x / 8;
+        t_end = (xcd + 1) * a.n_tiles / 8;
+        t_step = gridDim.x / 8;
+    }
+#endif
+    for (int64_t tile = t_begin; tile < t_end; tile += t_step) {
         const int64_t p_raw = tile * COLS + col;
         const int64_t p = p_raw < a.n_points ? p_raw : a.n_points - 1;
         float px, py, pz, dx, dy, dz;
@@ -971,6 +1003,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             else { dx = dy = dz = 0.f; }
             obj = p / a.points_per_obj;
         }
+        PT_WAIT();
+        PT(gc, 8);
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         float *xp = a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + lane * 4;
         float *xs = xp + COLS * H;
@@ -987,8 +1021,11 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 xc[i] = add_rn(xr[i], cam[9 + i]);
             }
             const float fx = cam[12], fy = cam[13], cx = cam[14], cy = cam[15];
+            PT_WAIT();
+            PT(gc, 9);
             // features f = FPT qt .. FPT qt + FPT - 1 of [xyz_rot | PE | viewdir_cam | 0]
             __syncthreads();   // previous users of inbuf are done
+            PT(gc, 10);
             {
                 const int npe = 3 * L.pe_n;
                 float fv[FPT];
@@ -1000,7 +1037,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     else if (f < 3 + npe) {
                         const int m = f - 3, q = m / 3, d = m - 3 * q;
                         const float xd = d == 0 ? xr[0] : (d == 1 ? xr[1] : xr[2]);
-                        val = sinf(add_rn(pe_p[q], mul_rn(xd, pe_f[q])));
+                        val = sinf(add_rn(petab[16 + q], mul_rn(xd, petab[q])));   // code._phases, _freqs
                     } else if (f < 6 + npe) {
                         const int d = f - 3 - npe;
                         val = d == 0 ? vd[0] : (d == 1 ? vd[1] : vd[2]);
@@ -1034,6 +1071,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                             f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
                 }
             }
+            PT(gc, 11);
             // projection (models.py:206-212) -> grid_sample coords (encoder.py:95-108)
             float u = mul_rn(__fdiv_rn(-xc[0], xc[2]), fx);
             float w = mul_rn(__fdiv_rn(-xc[1], xc[2]), fy);
@@ -1066,6 +1104,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                                 __uint_as_float(o10), __uint_as_float(o11)};
                 *reinterpret_cast<f4 *>(t + 4) = f4{wnw, wne, wsw, wse};
             }
+            PT(gc, 12);
             __syncthreads();   // features visible
             PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
@@ -1139,14 +1178,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 PT(gc, 1);
                 add_bias(x, bias + (1 + lz) * H, wave, g, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
-                __syncthreads();
+                pre_publish_sync();
                 }
                 publish_relu(x, tile, blk);
                 if constexpr (PREC != 0 && kParkX) park(x, xp);
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, g, false);
                 layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
-                __syncthreads();
+                pre_publish_sync();
                 publish_relu(h, tile, L.n_blocks + blk);
                 __syncthreads();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp);
@@ -1184,13 +1223,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         // ---- blocks after the combine layer ------------------------------------------
         for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
             const int l0 = layer_index(blk, 1, L.ncomb);
-            __syncthreads();
+            pre_publish_sync();
             publish_relu(x, tile, blk);
             if constexpr (PREC != 0 && kParkX) park(x, xp);
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, g, false);
             layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
-            __syncthreads();
+            pre_publish_sync();
             publish_relu(h, tile, L.n_blocks + blk);
             __syncthreads();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp);
@@ -1198,7 +1237,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
-        __syncthreads();
+        pre_publish_sync();
         publish_relu(x, tile, 2 * L.n_blocks);
         __syncthreads();
         PT(gc, 3);
@@ -1269,7 +1308,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     }
 #ifdef PNR_PHASE_TIMING
     if (threadIdx.x == 0)
-        for (int i = 0; i < 8; ++i) atomicAdd(&g_phase[i], (unsigned long long)gc.pt[i]);
+        for (int i = 0; i < PT_SLOTS; ++i) atomicAdd(&g_phase[i], (unsigned long long)gc.pt[i]);
 #endif
 }
 
@@ -1458,10 +1497,10 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
 #ifdef PNR_PHASE_TIMING
 // diagnostic: copy (and optionally clear) the phase counters; not part of the ABI
 extern "C" int pnr_debug_phase(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mlpk::g_phase), sizeof(unsigned long long) * 8) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mlpk::g_phase), sizeof(unsigned long long) * mlpk::PT_SLOTS) != hipSuccess)
         return -1;
     if (reset) {
-        static const unsigned long long zero[8] = {};
+        static const unsigned long long zero[mlpk::PT_SLOTS] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(mlpk::g_phase), zero, sizeof(zero)) != hipSuccess) return -1;
     }
     return 0;
@@ -1628,11 +1667,11 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.proj_stride = (int64_t)sc.n_obj * sc.n_views * sc.latent_h * sc.latent_w * mlpk::H;
     const int cus = device_cu_count();
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
-    // PREC 3: split image P0 + P1, gather records, column maxima, exponents = 139,520 B
-    // else:   fp32 activations + staging ring + gather records            = 158,720 B
+    // PREC 3: split image P0 + P1, gather records, column maxima, exponents, PE table = 143,744 B
+    // else:   fp32 activations + staging ring + gather records + PE table          = 158,848 B
     const size_t lds = d.precision == PNR_PREC_F16X3
-        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS)
-        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8);
+        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS + 32)
+        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8 + 32);
 #define PNR_LAUNCH_MLP(P)                                                                              \
     do {                                                                                               \
         if (proj) hipLaunchKernelGGL((mlpk::k_point_mlp<P, true>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \

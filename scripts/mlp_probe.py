@@ -22,7 +22,7 @@ import ctypes  # noqa: E402
 from pnr import _lib  # noqa: E402
 
 dbg = getattr(_lib.load(), "pnr_debug_phase", None)   # PNR_PHASE_TIMING variant only
-ph = (ctypes.c_ulonglong * 8)()
+ph = (ctypes.c_ulonglong * 16)()
 with torch.no_grad():
     r(net, rays[:4096][None])
     torch.cuda.synchronize()
@@ -37,11 +37,15 @@ print("done", prec, "proj" if net.use_latent_proj else "gather", n, "chunk_ms %.
 if dbg is not None:
     dbg(ph, 0)
     v = list(ph)
+    sub = ["ray/z loads", "cam loads + transform", "barrier A", "PE + split", "projection", "barrier B"]
+    subd = {nm: round(v[k] / max(v[6], 1)) for nm, k in zip(sub, [8, 9, 10, 11, 12, 0])}
+    v[0] += sum(v[8:13])   # the features phase is stamped in parts (slots 8-12 + 0)
     names = ["features", "gather", "gemm", "glue", "head"]
     tot = sum(v[:5])
     print("phase cycles/tile (wave 0):", {nm: round(v[i] / v[6]) for i, nm in enumerate(names)},
           "share:", {nm: round(v[i] / tot, 4) for i, nm in enumerate(names)},
           "gemm cycles/call: %.0f" % (v[2] / v[5]), "calls", v[5], "tiles", v[6])
+    print("features split (cycles/tile):", subd)
 
 if os.environ.get("COMPOSITE"):
     with torch.no_grad():
