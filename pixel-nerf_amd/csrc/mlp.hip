@@ -337,9 +337,19 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
 
 typedef f4 Acc[RTW][CT];
 
+// The lane index through an empty asm: per-lane LDS / global addresses derived from it are
+// recomputed at each inlined use instead of hoisted out of the tile loop, where the 256
+// registers of a wave at 2 waves per SIMD turned them into scratch spills whose reloads
+// each cost a memory latency.
+__device__ __forceinline__ int opaque_lane(int lane) {
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
+
 // relu(acc) of this wave's rows -> save slot [point][512] (points of this tile < n_points)
 __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -360,6 +370,7 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
 __device__ __forceinline__ void save_mask(const Acc &acc, uint32_t *mslot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
     static_assert(RTW == 4, "mask bytes assume 4 row tiles per wave");
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
     auto nib = [](const f4 &v) {
         return (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) | (v.w > 0.f ? 8u : 0u);
@@ -664,6 +675,7 @@ __device__ __forceinline__ void put_split4(_Float16 *P0, _Float16 *P1, int off, 
 // relu(acc) (RELU) or |acc| of this wave's rows -> per-column partial maxima cmax[column][wave slot]
 template <bool RELU = true>
 __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wave, int lane) {
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -688,6 +700,7 @@ __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wav
 template <bool RELU = true>
 __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
                                                  const float *cmax, int *ecol, int wave, int lane) {
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -708,8 +721,9 @@ __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _
 }
 
 // acc = bias (per output row) [+ acc]
-__device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bias, int wave, int g,
+__device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bias, int wave, int lane,
                                          bool accumulate) {
+    const int g = opaque_lane(lane) >> 4;
 #pragma unroll
     for (int r = 0; r < RTW; ++r) {
 #ifdef PNR_ABLATE_BIAS
@@ -804,7 +818,7 @@ __device__ __forceinline__ void stage_proj(float *stage, const float *__restrict
         const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-            const uint32_t ch = half * 256 + lane * 4;
+            const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
 #ifdef PNR_ABLATE_GATHER
             const f4 c0 = tw, c1 = to, c2 = tw, c3 = to;   // diagnostic: no loads
 #else
@@ -826,6 +840,7 @@ static_assert(sizeof(float) * COLS * LDS_LD <= 2 * sizeof(_Float16) * PART_HALVE
               "the fp32 stage fits in the split image it aliases");
 // x[r][c] += stage rows of this wave (column 16c + cl, rows 16 (RTW wave + r) + 4g ..)
 __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, int lane) {
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int r = 0; r < RTW; ++r)
@@ -849,7 +864,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
     } else if constexpr (PREC == 3) {
         // the accumulators run in the products' scale 2^(eW + e_col): exact for powers of
         // two, so the fp32 rounding sequence is that of the unscaled sum
-        const int cl = g.lane & 15;
+        const int cl = opaque_lane(g.lane) & 15;
         const int ew = (int)g.hdr[HDR_ESCALE + hidx];
         float sa[CT], ia[CT];
 #pragma unroll
@@ -919,7 +934,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
     // feature role: thread -> (column col, part qt of WAVES); FPT features each
     constexpr int FPT = 64 / WAVES;
-    const int col = tid / WAVES, qt = tid % WAVES;
 
     // relu(acc) -> the next GEMM's input image (callers barrier before and after)
     // activation save slots (training forward)
@@ -983,33 +997,38 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     }
 #endif
     for (int64_t tile = t_begin; tile < t_end; tile += t_step) {
+        const int tid_t = opaque_lane(tid);   // per-tile: keeps the feature addresses out of scratch
+        const int col = tid_t / WAVES, qt = tid_t % WAVES;
         const int64_t p_raw = tile * COLS + col;
         const int64_t p = p_raw < a.n_points ? p_raw : a.n_points - 1;
-        float px, py, pz, dx, dy, dz;
-        int64_t obj;
-        if (a.render_mode) {
-            const int64_t b = p / a.K;
-            const float *ray = a.rays + b * 8;
-            const float zz = a.zs[p];
-            dx = ray[3]; dy = ray[4]; dz = ray[5];
-            // points = o + z * d  (nerf.py:185)
-            px = add_rn(ray[0], mul_rn(zz, dx));
-            py = add_rn(ray[1], mul_rn(zz, dy));
-            pz = add_rn(ray[2], mul_rn(zz, dz));
-            obj = b / a.rays_per_obj;
-        } else {
-            px = a.xyz[p * 3 + 0]; py = a.xyz[p * 3 + 1]; pz = a.xyz[p * 3 + 2];
-            if (a.dirs) { dx = a.dirs[p * 3 + 0]; dy = a.dirs[p * 3 + 1]; dz = a.dirs[p * 3 + 2]; }
-            else { dx = dy = dz = 0.f; }
-            obj = p / a.points_per_obj;
-        }
-        PT_WAIT();
-        PT(gc, 8);
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
-        float *xp = a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + lane * 4;
-        float *xs = xp + COLS * H;
+        // (addresses formed at use: nothing per tile stays live across the GEMMs)
+        auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + lane * 4; };
+        auto xs_ptr = [&]() { return xp_ptr() + COLS * H; };
 
         for (int v = 0; v < a.ns; ++v) {
+            // the point (re-read per view from L2 rather than held in registers across the
+            // per-view blocks' GEMMs)
+            float px, py, pz, dx, dy, dz;
+            int64_t obj;
+            if (a.render_mode) {
+                const int64_t b = p / a.K;
+                const float *ray = a.rays + b * 8;
+                const float zz = a.zs[p];
+                dx = ray[3]; dy = ray[4]; dz = ray[5];
+                // points = o + z * d  (nerf.py:185)
+                px = add_rn(ray[0], mul_rn(zz, dx));
+                py = add_rn(ray[1], mul_rn(zz, dy));
+                pz = add_rn(ray[2], mul_rn(zz, dz));
+                obj = b / a.rays_per_obj;
+            } else {
+                px = a.xyz[p * 3 + 0]; py = a.xyz[p * 3 + 1]; pz = a.xyz[p * 3 + 2];
+                if (a.dirs) { dx = a.dirs[p * 3 + 0]; dy = a.dirs[p * 3 + 1]; dz = a.dirs[p * 3 + 2]; }
+                else { dx = dy = dz = 0.f; }
+                obj = p / a.points_per_obj;
+            }
+            PT_WAIT();
+            PT(gc, 8);
             // ---- per (point, view) geometry (this thread's column) ----------------
             const float *cam = a.cams + (obj * a.ns + v) * 16;
             float xr[3], vd[3], xc[3];
@@ -1108,7 +1127,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             __syncthreads();   // features visible
             PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
-            add_bias(x, bias, wave, g, false);
+            add_bias(x, bias, wave, lane, false);
             layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, gc, 0);
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
@@ -1121,7 +1140,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     stage_proj(inbuf, a.proj + blk * a.proj_stride, gtab, wave, lane);
                     __syncthreads();
                     PT(gc, 1);
-                    add_bias(x, bias + (1 + lz) * H, wave, g, true);
+                    add_bias(x, bias + (1 + lz) * H, wave, lane, true);
                     add_stage(x, inbuf, wave, lane);
                 } else {
                 __syncthreads();
@@ -1176,24 +1195,25 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 }
                 __syncthreads();
                 PT(gc, 1);
-                add_bias(x, bias + (1 + lz) * H, wave, g, true);
+                add_bias(x, bias + (1 + lz) * H, wave, lane, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 pre_publish_sync();
                 }
                 publish_relu(x, tile, blk);
-                if constexpr (PREC != 0 && kParkX) park(x, xp);
+                if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 __syncthreads();
-                add_bias(h, bias + (2 + lz) * H, wave, g, false);
+                add_bias(h, bias + (2 + lz) * H, wave, lane, false);
                 layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
                 pre_publish_sync();
                 publish_relu(h, tile, L.n_blocks + blk);
                 __syncthreads();
-                if constexpr (PREC != 0 && kParkX) unpark(x, xp);
-                add_bias(x, bias + (3 + lz) * H, wave, g, true);
+                if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
+                add_bias(x, bias + (3 + lz) * H, wave, lane, true);
                 layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
+                float *xs = xs_ptr();
                 if (v == 0) {
 #pragma unroll
                     for (int r = 0; r < RTW; ++r)
@@ -1225,15 +1245,15 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             pre_publish_sync();
             publish_relu(x, tile, blk);
-            if constexpr (PREC != 0 && kParkX) park(x, xp);
+            if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
             __syncthreads();
-            add_bias(h, bias + (1 + l0) * H, wave, g, false);
+            add_bias(h, bias + (1 + l0) * H, wave, lane, false);
             layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
             pre_publish_sync();
             publish_relu(h, tile, L.n_blocks + blk);
             __syncthreads();
-            if constexpr (PREC != 0 && kParkX) unpark(x, xp);
-            add_bias(x, bias + (2 + l0) * H, wave, g, true);
+            if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
+            add_bias(x, bias + (2 + l0) * H, wave, lane, true);
             layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
