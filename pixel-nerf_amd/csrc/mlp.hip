@@ -877,7 +877,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
-        gemm_f16<NK / 2>(acc, layer_base + g.ws_off, g.pb0, g.pb1);
+        gemm_f16<NK / 2>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -997,16 +997,17 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     }
 #endif
     for (int64_t tile = t_begin; tile < t_end; tile += t_step) {
-        const int tid_t = opaque_lane(tid);   // per-tile: keeps the feature addresses out of scratch
-        const int col = tid_t / WAVES, qt = tid_t % WAVES;
-        const int64_t p_raw = tile * COLS + col;
-        const int64_t p = p_raw < a.n_points ? p_raw : a.n_points - 1;
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         // (addresses formed at use: nothing per tile stays live across the GEMMs)
         auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + lane * 4; };
         auto xs_ptr = [&]() { return xp_ptr() + COLS * H; };
 
         for (int v = 0; v < a.ns; ++v) {
+            // per view: keeps the feature addresses out of scratch across the GEMMs
+            const int tid_t = opaque_lane(tid);
+            const int col = tid_t / WAVES, qt = tid_t % WAVES;
+            const int64_t p_raw = tile * COLS + col;
+            const int64_t p = p_raw < a.n_points ? p_raw : a.n_points - 1;
             // the point (re-read per view from L2 rather than held in registers across the
             // per-view blocks' GEMMs)
             float px, py, pz, dx, dy, dz;
