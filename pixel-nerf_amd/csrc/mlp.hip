@@ -1160,7 +1160,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     f4 zh[2];
 #pragma unroll
                     for (int half = 0; half < 2; ++half) {
-                        const uint32_t ch = half * 256 + lane * 4;
+                        const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
 #ifdef PNR_ABLATE_GATHER
                         const f4 c0 = tw, c1 = to, c2 = tw, c3 = to;  // diagnostic
 #else
@@ -1363,6 +1363,7 @@ struct BwdArgs {
 // this wave's rows of acc -> slot [point][512] (points < n_points)
 __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
                                            int wave, int lane) {
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -1378,7 +1379,7 @@ __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t 
 typedef unsigned u2m __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void load_mask(u2m (&mk)[CT], const uint32_t *mslot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
-    const int cl = lane & 15;
+    const int cl = opaque_lane(lane) & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
@@ -1389,6 +1390,7 @@ __device__ __forceinline__ void load_mask(u2m (&mk)[CT], const uint32_t *mslot, 
 // acc *= [activation > 0] (torch's relu backward); 0 past n_points
 __device__ __forceinline__ void relu_mask(Acc &acc, const u2m (&mk)[CT], int64_t tile, int64_t n_points,
                                           int lane) {
+    lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
@@ -1433,7 +1435,8 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     u2m mk[CT];
     auto dy_slot = [&](int i) { return a.dy + P * H * i; };
     auto publish = [&](const Acc &acc) {
-        __syncthreads();   // the previous image's readers are done
+        // no barrier first: the column maxima are written before the internal barrier and the
+        // image after it, when every wave has left the GEMM that read the previous image
         relu_colmax<false>(acc, cmax, wave, lane);
         __syncthreads();
         relu_store_split<false>(acc, P0, P1, cmax, ecol, wave, lane);
@@ -1496,11 +1499,12 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                 const bool first = b == L.n_linz - 1;
 #pragma unroll
                 for (int c = 0; c < CT; ++c) {
-                    const int64_t p = tile * COLS + 16 * c + cl;
+                    const int ln = opaque_lane(lane), gz = ln >> 4;
+                    const int64_t p = tile * COLS + 16 * c + (ln & 15);
                     if (p >= P) continue;
 #pragma unroll
                     for (int r = 0; r < RTW; ++r) {
-                        f4 *q = reinterpret_cast<f4 *>(a.dzlat + p * H + 16 * (RTW * wave + r) + 4 * g);
+                        f4 *q = reinterpret_cast<f4 *>(a.dzlat + p * H + 16 * (RTW * wave + r) + 4 * gz);
                         *q = first ? h[r][c] : *q + h[r][c];
                     }
                 }
