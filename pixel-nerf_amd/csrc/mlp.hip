@@ -806,36 +806,55 @@ struct GemmCtx {
 // LDS as fp32 stage[column][LDS_LD]: resnetfc.py:160-163 on grid_sample's blend
 // (encoder.py:102-108), evaluated by linearity as the blend of four rows of the projected
 // latent P = latent W_z^T (proj.hip), torch's nw, ne, sw, se summation order.  Wave w blends
-// the COLS / WAVES columns [8w, 8w + 8); each load instruction reads one contiguous 1 KB half
-// of a corner's 2 KB row.  Callers barrier before (the stage aliases the GEMM input image)
-// and after.
-__device__ __forceinline__ void stage_proj(float *stage, const float *__restrict__ pz, const float *gtab, int wave,
-                                           int lane) {
-#pragma unroll 4
-    for (int j = 0; j < COLS / WAVES; ++j) {
-        const int cj = (COLS / WAVES) * wave + j;
+// the COLS / WAVES columns [8w, 8w + 8), in two batches of 4; each load instruction reads one
+// contiguous 1 KB half of a corner's 2 KB row.  The stage aliases the GEMM input image, so
+// the first batch's loads are issued BEFORE the barrier that frees it (proj_load) and land
+// while the wave waits for its SIMD-mate's GEMM; blends and LDS writes come after.
+constexpr int PJ = 4;   // columns per batch
+struct ProjRows {
+    f4 c[PJ][2][4];     // [column][channel half][corner]
+    f4 tw[PJ];          // bilinear weights nw, ne, sw, se
+};
+__device__ __forceinline__ void proj_load(ProjRows &R, const float *__restrict__ pz, const float *gtab, int j0,
+                                          int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+        const int cj = (COLS / WAVES) * wave + j0 + j;
         const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
-        const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
+        R.tw[j] = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
             const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
 #ifdef PNR_ABLATE_GATHER
-            const f4 c0 = tw, c1 = to, c2 = tw, c3 = to;   // diagnostic: no loads
+            R.c[j][half][0] = R.c[j][half][1] = R.c[j][half][2] = R.c[j][half][3] = to;   // diagnostic: no loads
 #else
-            const f4 c0 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.x) + ch);
-            const f4 c1 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.y) + ch);
-            const f4 c2 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.z) + ch);
-            const f4 c3 = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.w) + ch);
+            R.c[j][half][0] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.x) + ch);
+            R.c[j][half][1] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.y) + ch);
+            R.c[j][half][2] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.z) + ch);
+            R.c[j][half][3] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.w) + ch);
 #endif
+        }
+    }
+}
+__device__ __forceinline__ void proj_blend_store(const ProjRows &R, float *stage, int j0, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < PJ; ++j) {
+        const int cj = (COLS / WAVES) * wave + j0 + j;
+        const f4 tw = R.tw[j];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
+            const f4 *c = R.c[j][half];
             f4 zz;
 #pragma unroll
             for (int q = 0; q < 4; ++q)
-                zz[q] = add_rn(add_rn(add_rn(mul_rn(c0[q], tw.x), mul_rn(c1[q], tw.y)), mul_rn(c2[q], tw.z)),
-                               mul_rn(c3[q], tw.w));
+                zz[q] = add_rn(add_rn(add_rn(mul_rn(c[0][q], tw.x), mul_rn(c[1][q], tw.y)), mul_rn(c[2][q], tw.z)),
+                               mul_rn(c[3][q], tw.w));
             *reinterpret_cast<f4 *>(stage + cj * LDS_LD + ch) = zz;
         }
     }
 }
+static_assert(2 * PJ == COLS / WAVES, "two batches cover a wave's columns");
 static_assert(sizeof(float) * COLS * LDS_LD <= 2 * sizeof(_Float16) * PART_HALVES,
               "the fp32 stage fits in the split image it aliases");
 // x[r][c] += stage rows of this wave (column 16c + cl, rows 16 (RTW wave + r) + 4g ..)
@@ -1136,9 +1155,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 if constexpr (PZ) {
                     // the stage aliases the image the previous GEMM read; publish_relu's
                     // internal barrier orders the add_stage reads before the image writes
+                    const float *pz = a.proj + blk * a.proj_stride;
+                    ProjRows rows;
+                    proj_load(rows, pz, gtab, 0, wave, lane);
                     __syncthreads();
                     PT(gc, 3);
-                    stage_proj(inbuf, a.proj + blk * a.proj_stride, gtab, wave, lane);
+                    proj_blend_store(rows, inbuf, 0, wave, lane);
+                    proj_load(rows, pz, gtab, PJ, wave, lane);
+                    proj_blend_store(rows, inbuf, PJ, wave, lane);
                     __syncthreads();
                     PT(gc, 1);
                     add_bias(x, bias + (1 + lz) * H, wave, lane, true);
