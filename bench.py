@@ -265,6 +265,13 @@ def extra_configs(dev, precision, latent_proj=True):
     s = _time_render(net, r, rays, CHUNK)
     res["cfg2_shipped_64_32_16"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
                                         gflop_per_ray=round(160 * FLOP_PER_POINT_NS1 / 1e9, 4))
+    # cfg2 as eval_approx.py --coarse renders it: mlp_fine = None, 64 + 128 samples (the fine
+    # pass reuses the coarse pass's outputs for the 64 coarse samples)
+    net.mlp_fine = None
+    r = NeRFRenderer(n_coarse=64, n_fine=128, white_bkgd=True).to(dev)
+    s = _time_render(net, r, rays, CHUNK)
+    res["cfg2_coarse_as_fine_64_128"] = dict(rays_per_s=round(rays.shape[0] / s, 1),
+                                             ms_per_frame=round(s * 1e3, 3))
     # cfg3, NMR 64x64: 24 target views of one object
     net = make(synth.latent(3, 1, 512, 32, 32), synth.srn_poses([0.0], radius=2.7), torch.tensor(70.0), (64, 64))
     rays = util.gen_rays(synth.srn_poses([15.0 * i for i in range(24)], radius=2.7).to(dev), 64, 64,

@@ -197,7 +197,10 @@ int pnr_latent_project(const pnr_scene *scene, const pnr_mlp_weights *w, float *
 /* pnr_point_query / pnr_render_forward_events with the projected latent of the model(s):
  * `proj` (point query), `coarse_proj` / `fine_proj` (render; pass the coarse projection
  * twice when mlp_fine is None) from pnr_latent_project on the same scene and weights.
- * NULL projections select the latent gather + lin_z GEMM path.  `events` may be NULL. */
+ * NULL projections select the latent gather + lin_z GEMM path.  `events` may be NULL.
+ * When fine_packed == coarse_packed and fine_proj == coarse_proj (mlp_fine is None), the fine
+ * pass evaluates only the n_fine new samples and reuses the coarse pass's outputs for the
+ * n_coarse coarse samples (bit-identical: a point's output does not depend on the others). */
 int pnr_point_query_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
                          const float *proj, const float *xyz, const float *viewdirs,
                          int64_t points_per_obj, float *out, void *workspace,

@@ -14,7 +14,8 @@ namespace pnr {
 int launch_sample_coarse(const float *, int64_t, int, const float *, int, float *, hipStream_t);
 int launch_sample_fine(const float *, int64_t, int, const float *, const float *, const float *,
                        int, int, float, const float *, const float *, const float *, int, float *,
-                       hipStream_t);
+                       hipStream_t, int *origin = nullptr, float *z_new = nullptr);
+int launch_merge_raw(const int *, const float *, const float *, int64_t, int, int, float *, hipStream_t);
 int launch_gen_rays(const float *, int64_t, int, int, int, float, float, float, float, float, float,
                     float *, hipStream_t);
 int launch_composite(const float *, const float *, const float *, int64_t, int, int, float *,
@@ -265,7 +266,7 @@ int pnr_weight_grad(const float *const *dy, const float *const *x, float *const 
 
 // workspace layout of pnr_render_forward
 struct RenderWs {
-    size_t z_c, raw_c, w_c, z_f, raw_f, xsum, total;
+    size_t z_c, raw_c, w_c, z_f, raw_f, xsum, origin, z_new, raw_new, total;
 };
 
 static RenderWs render_ws(const pnr_scene *sc, const pnr_render_cfg *cfg, int64_t n) {
@@ -278,6 +279,11 @@ static RenderWs render_ws(const pnr_scene *sc, const pnr_render_cfg *cfg, int64_
     w.z_f = o; o += cfg->n_fine > 0 ? align_up(sizeof(float) * n * kall) : 0;
     w.raw_f = o; o += cfg->n_fine > 0 ? align_up(sizeof(float) * n * kall * 4) : 0;
     w.xsum = o; o += align_up(mlp_xsum_bytes(sc->n_views));
+    // coarse-output reuse when the fine pass runs the coarse MLP (see pnr_render_forward_proj)
+    const size_t kf = (size_t)cfg->n_fine;
+    w.origin = o; o += kf > 0 ? align_up(sizeof(int) * n * kall) : 0;
+    w.z_new = o; o += kf > 0 ? align_up(sizeof(float) * n * kf) : 0;
+    w.raw_new = o; o += kf > 0 ? align_up(sizeof(float) * n * kf * 4) : 0;
     w.total = o;
     return w;
 }
@@ -364,13 +370,26 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     const int kall = kc + kf;
     float *zf = out->z_fine ? out->z_fine : reinterpret_cast<float *>(ws + w.z_f);
     float *rawf = reinterpret_cast<float *>(ws + w.raw_f);
+    // mlp_fine is None (the coarse pack passed twice, models.py:242-255; eval_approx.py --coarse):
+    // the kc coarse samples re-enter the fine pass with the MLP that already evaluated them, so
+    // only the kf new samples run through it and the coarse outputs are merged in.
+    const bool reuse = fine_packed == coarse_packed && fine_proj == coarse_proj;
+    int *origin = reuse ? reinterpret_cast<int *>(ws + w.origin) : nullptr;
+    float *z_new = reuse ? reinterpret_cast<float *>(ws + w.z_new) : nullptr;
     if ((rc = launch_sample_fine(rays->rays, n, kc, zc, wc, out->coarse_depth, kf, kfd, cfg->depth_std,
-                                 rng->u_fine, rng->u_fine_jit, rng->n_depth, cfg->lindisp, zf, st)))
+                                 rng->u_fine, rng->u_fine_jit, rng->n_depth, cfg->lindisp, zf, st, origin, z_new)))
         return rc;
     if ((rc = mark(4))) return rc;
-    if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, zf, kall, rays->rays_per_obj,
-                               nullptr, nullptr, 1, n * kall, rawf, xsum, st, nullptr, fine_proj)))
+    if (reuse) {
+        float *raw_new = reinterpret_cast<float *>(ws + w.raw_new);
+        if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, z_new, kf, rays->rays_per_obj,
+                                   nullptr, nullptr, 1, n * kf, raw_new, xsum, st, nullptr, fine_proj)))
+            return rc;
+        if ((rc = launch_merge_raw(origin, rawc, raw_new, n, kc, kf, rawf, st))) return rc;
+    } else if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, zf, kall, rays->rays_per_obj,
+                                      nullptr, nullptr, 1, n * kall, rawf, xsum, st, nullptr, fine_proj))) {
         return rc;
+    }
     if ((rc = mark(5))) return rc;
     if ((rc = launch_composite(zf, rawf, rays->rays, n, kall, cfg->white_bkgd, out->fine_weights,
                                out->fine_rgb, out->fine_depth, st)))

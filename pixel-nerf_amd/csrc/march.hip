@@ -44,10 +44,12 @@ __global__ __launch_bounds__(64) void k_sample_fine(
     const float *__restrict__ rays, int kc, const float *__restrict__ z_coarse,
     const float *__restrict__ weights, const float *__restrict__ depth, int kf, int kfd,
     float depth_std, const float *__restrict__ u_fine, const float *__restrict__ u_jit,
-    const float *__restrict__ n_depth, int lindisp, int n_sort, float *__restrict__ z_fine) {
+    const float *__restrict__ n_depth, int lindisp, int n_sort, float *__restrict__ z_fine,
+    int *__restrict__ origin, float *__restrict__ z_new) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *cdf = smem;            // kc + 1
     float *s = smem + kc + 1;     // n_sort (power of two >= kc + kf)
+    int *si = reinterpret_cast<int *>(s + n_sort);   // origin of each sorted value (origin != NULL)
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
     const float near = rays[b * 8 + 6], far = rays[b * 8 + 7];
@@ -97,6 +99,11 @@ __global__ __launch_bounds__(64) void k_sample_fine(
     for (int k = lane; k < kc; k += 64) s[k] = z_coarse[b * kc + k];
     for (int k = kc + kf + lane; k < n_sort; k += 64) s[k] = __builtin_inff();
     __syncthreads();
+    if (origin) {   // the new samples in draw order, and every value's index in cat(coarse, new)
+        for (int j = lane; j < kf; j += 64) z_new[b * kf + j] = s[kc + j];
+        for (int k = lane; k < n_sort; k += 64) si[k] = k;
+        __syncthreads();
+    }
     // bitonic sort of n_sort values, ascending (torch.sort, nerf.py:295)
     for (int size = 2; size <= n_sort; size <<= 1) {
         for (int j = size >> 1; j > 0; j >>= 1) {
@@ -105,13 +112,33 @@ __global__ __launch_bounds__(64) void k_sample_fine(
                 const int hi = lo + j;
                 const bool asc = (lo & size) == 0;
                 float a = s[lo], c = s[hi];
-                if ((a > c) == asc) { s[lo] = c; s[hi] = a; }
+                if ((a > c) == asc) {
+                    s[lo] = c; s[hi] = a;
+                    if (origin) { const int t0 = si[lo]; si[lo] = si[hi]; si[hi] = t0; }
+                }
             }
             __syncthreads();
         }
     }
     const int k_all = kc + kf;
     for (int k = lane; k < k_all; k += 64) z_fine[b * k_all + k] = s[k];
+    if (origin)
+        for (int k = lane; k < k_all; k += 64) origin[b * k_all + k] = si[k];
+}
+
+// raw_f[b][k] = raw of sorted fine sample k: the coarse pass's output for a coarse sample
+// (origin < kc), the new-sample evaluation otherwise.  Used when the fine pass runs the
+// coarse MLP (mlp_fine is None, models.py:242-255): its kc coarse points were already
+// evaluated, bit-identically (a point's output does not depend on its tile neighbours).
+__global__ __launch_bounds__(256) void k_merge_raw(const int *__restrict__ origin, const f4 *__restrict__ raw_c,
+                                                   const f4 *__restrict__ raw_new, int64_t n, int kc, int kf,
+                                                   f4 *__restrict__ raw_f) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int k_all = kc + kf;
+    const int64_t b = i / k_all;
+    const int o = origin[i];
+    raw_f[i] = o < kc ? raw_c[b * kc + o] : raw_new[b * kf + (o - kc)];
 }
 
 // ---------------------------------------------------------------------------
@@ -319,14 +346,25 @@ int sort_width(int n) {
 int launch_sample_fine(const float *rays, int64_t n_rays, int kc, const float *z_coarse,
                        const float *weights, const float *depth, int kf, int kfd,
                        float depth_std, const float *u_fine, const float *u_jit,
-                       const float *n_depth, int lindisp, float *z_fine, hipStream_t st) {
+                       const float *n_depth, int lindisp, float *z_fine, hipStream_t st,
+                       int *origin, float *z_new) {
     if (n_rays == 0) return PNR_OK;
     const int n_sort = sort_width(kc + kf);
-    const size_t lds = sizeof(float) * (size_t)(kc + 1 + n_sort);
+    const size_t lds = sizeof(float) * (size_t)(kc + 1 + (origin ? 2 : 1) * n_sort);
     hipLaunchKernelGGL(k_sample_fine, dim3((unsigned)n_rays), dim3(64), lds, st, rays, kc,
                        z_coarse, weights, depth, kf, kfd, depth_std, u_fine, u_jit, n_depth,
-                       lindisp, n_sort, z_fine);
+                       lindisp, n_sort, z_fine, origin, z_new);
     return launch_ok("sample_fine") ? PNR_OK : PNR_ERR_HIP;
+}
+
+int launch_merge_raw(const int *origin, const float *raw_c, const float *raw_new, int64_t n_rays, int kc, int kf,
+                     float *raw_f, hipStream_t st) {
+    const int64_t n = n_rays * (kc + kf);
+    if (n == 0) return PNR_OK;
+    hipLaunchKernelGGL(k_merge_raw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, origin,
+                       reinterpret_cast<const f4 *>(raw_c), reinterpret_cast<const f4 *>(raw_new), n, kc, kf,
+                       reinterpret_cast<f4 *>(raw_f));
+    return launch_ok("merge_raw") ? PNR_OK : PNR_ERR_HIP;
 }
 
 int launch_composite(const float *z, const float *raw, const float *rays, int64_t n_rays, int K,

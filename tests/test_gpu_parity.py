@@ -488,3 +488,52 @@ def test_latent_channels_last_matches_torch_upsample_concat():
     # grad, so the comparison carries the convolutions' own fp32 spread (upsample checked above)
     torch.testing.assert_close(lat_hip, lat_torch.detach(), atol=1e-4, rtol=1e-5)
     torch.testing.assert_close(cl_hip, enc.latent_cl.detach(), atol=1e-4, rtol=1e-5)
+
+
+# ----------------------------------------------------- coarse-output reuse --
+@pytest.mark.parametrize("kfd", [0, 16])
+def test_fine_pass_reuses_coarse_outputs_when_mlp_fine_is_none(kfd):
+    """eval_approx.py --coarse: mlp_fine = None, 64 coarse + 128 fine samples.  The fine pass
+    then runs the coarse MLP, so pnr_render_forward_proj evaluates only the new samples and
+    merges the coarse pass's outputs.  The result must be BITWISE equal to a render whose fine
+    MLP is a separate copy of the coarse one (no reuse), and match the oracle."""
+    import copy
+
+    sd = synth.pixelnerf_state(3)
+    sc = synth.scene_srn(seed=4, n_rays=96, pick="hash")
+    streams = synth.rng_streams(6, 96, 64, 128, kfd)
+
+    def make(share):
+        net = PixelNeRFNet(model_conf())
+        net.load_state_dict(sd, strict=False)
+        if share:
+            net.mlp_fine = None
+        else:
+            net.mlp_fine = copy.deepcopy(net.mlp_coarse)
+        net = net.to(DEV).eval()
+        net.encode_latent(sc["latent"].to(DEV), sc["poses"].to(DEV), sc["focal"].to(DEV), (128, 128))
+        return net
+
+    outs = []
+    for share in (True, False):
+        r = NeRFRenderer(n_coarse=64, n_fine=128, n_fine_depth=kfd, white_bkgd=True)
+        r.streams = streams
+        with torch.no_grad():
+            outs.append(r(make(share), sc["rays"][None].to(DEV), want_weights=True))
+    torch.cuda.synchronize()
+    for part in ("coarse", "fine"):
+        for k in ("rgb", "depth", "weights"):
+            assert torch.equal(outs[0][part][k], outs[1][part][k]), (part, k)
+    # oracle: the coarse MLP in both passes
+    sd_c = dict(sd)
+    for k in list(sd):
+        if k.startswith("mlp_fine."):
+            sd_c[k] = sd["mlp_coarse." + k[len("mlp_fine."):]]
+    scene = ref_cpu.Scene(sc["latent"], sc["poses"], sc["focal"], 128, 128, None)
+    with torch.no_grad():
+        ref = ref_cpu.render(lambda p, c, d: ref_cpu.pixelnerf_forward(sd_c, scene, p, c, d),
+                             sc["rays"][None], 64, 128, kfd, streams, True)
+    arr = dict(coarse_rgb=ref["coarse"]["rgb"], coarse_depth=ref["coarse"]["depth"],
+               coarse_weights=ref["coarse"]["weights"], fine_rgb=ref["fine"]["rgb"],
+               fine_depth=ref["fine"]["depth"], fine_weights=ref["fine"]["weights"], z_fine=ref["fine"]["z"])
+    compare_render("reuse kfd=%d" % kfd, outs[0], dict(n_fine=128), arr)
