@@ -293,6 +293,30 @@ def extra_configs(dev, precision, latent_proj=True):
     return res
 
 
+L2_SHARED_READ_TBS = 18.8   # MI355X_MICROARCH.md: rows shared by every workgroup, read from the
+                            # XCD's L2 (66-73 GB/s per CU, 16.8-18.8 TB/s chip-wide, measured)
+
+
+def l2_stream(points, launch_ms, precision, latent_proj):
+    """The fused MLP's second roofline: every 64-point tile streams the whole packed network
+    from L2 (each CU reads each weight fragment once per tile) plus, with the projected
+    latent, three 4-corner blends of 2 KB rows per point.  Bytes per launch / launch time
+    against the guide's measured shared-L2 read rate."""
+    if precision != "f16x3":
+        return None
+    tiles = (points + 63) // 64
+    # packed 512x512 layers (10, or 13 with the per-point lin_z GEMMs), lin_in, lin_out
+    weights = (10 if latent_proj else 13) * (1 << 20) + (128 << 10) + (32 << 10)
+    gather = 3 * 64 * 4 * 2048   # 3 blends x 64 points x 4 corners x 2 KB rows (P or the latent)
+    total = tiles * (weights + gather)
+    tbs = total / (launch_ms * 1e-3) / 1e12
+    return {"kernel": "k_point_mlp (fine pass)", "bytes_per_tile": weights + gather, "tiles": tiles,
+            "achieved": round(tbs, 2), "peak": L2_SHARED_READ_TBS, "unit": "TB/s (L2 -> CU)",
+            "frac": round(tbs / L2_SHARED_READ_TBS, 4),
+            "note": "packed weight fragments per 64-point tile + 4-corner latent rows; peak is the "
+                    "guide's measured shared-L2 read rate, not a spec"}
+
+
 def pmc_traffic(kernel, render_pass):
     """Mean HBM bytes per launch of `kernel` in `render_pass` ("fine" / "coarse") from the
     newest committed PMC summary that has it (rocprofv3 counters cannot be read live from
@@ -460,6 +484,7 @@ def main():
                      "flop_per_launch": flop_fine,
                      "launch_ms": round(avg["mlp_fine"], 4)},
         "kernel_ms": {n: round(v, 4) for n, v in avg.items()},
+        "l2_stream": l2_stream(pts_fine, avg["mlp_fine"], args.precision, net.use_latent_proj),
     }
     if rank == 0 and world == 1 and not args.no_composite:
         out["composite"] = composite_roofline(dev, ev)
