@@ -1018,7 +1018,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     for (int64_t tile = t_begin; tile < t_end; tile += t_step) {
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         // (addresses formed at use: nothing per tile stays live across the GEMMs)
-        auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + lane * 4; };
+        auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + opaque_lane(lane) * 4; };
         auto xs_ptr = [&]() { return xp_ptr() + COLS * H; };
 
         for (int v = 0; v < a.ns; ++v) {
