@@ -318,6 +318,8 @@ struct Args {
     // (n_obj * n_views, H_l, W_l, 512) like the latent
     const float *proj;
     int64_t proj_stride;
+    // dynamic tile scheduling: 8 per-XCD tile counters, 64 B apart (zeroed per launch)
+    int *tile_ctr;
 };
 
 // floats of the activation save per point (Args::save): the fp32 regions, then the relu
@@ -1002,20 +1004,29 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     __syncthreads();
 #endif
     Acc x, h;
-    // XCD-aware tile order: workgroups are placed round-robin on the 8 XCDs (blockIdx.x % 8),
-    // so XCD x walks the contiguous tile range [x T / 8, (x + 1) T / 8).  Neighbouring tiles
-    // are neighbouring rays, which sample neighbouring latent pixels: each XCD's L2 then holds
-    // its own band of the (projected) latent instead of all of it.
-    int64_t t_begin = blockIdx.x, t_end = a.n_tiles, t_step = gridDim.x;
-#ifndef PNR_PLAIN_TILE_ORDER
-    if (gridDim.x % 8 == 0) {
-        const int64_t xcd = blockIdx.x % 8;
-        t_begin = xcd * a.n_tiles / 8 + blockIdx.x / 8;
-        t_end = (xcd + 1) * a.n_tiles / 8;
-        t_step = gridDim.x / 8;
-    }
-#endif
-    for (int64_t tile = t_begin; tile < t_end; tile += t_step) {
+    // Dynamic, XCD-aware tile order.  Workgroups are placed round-robin on the 8 XCDs
+    // (blockIdx.x % 8); XCD x owns the contiguous tile range [x T / 8, (x + 1) T / 8)
+    // (neighbouring tiles are neighbouring rays, which sample neighbouring latent pixels, so
+    // each XCD's L2 holds its own band of the projected latent).  Its workgroups take tiles
+    // from that range through an atomic counter and, once it is empty, from the other XCDs'
+    // ranges: a slower CU or XCD no longer leaves the rest of the chip idle at the end of
+    // the launch.  The next tile is fetched before the head, so the atomic's latency hides.
+    int *s_next = reinterpret_cast<int *>(petab + 32);
+    auto grab = [&]() -> int {
+        const int64_t T = a.n_tiles;
+        const int x0 = blockIdx.x & 7;
+        for (int k = 0; k < 8; ++k) {
+            const int x = (x0 + k) & 7;
+            const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
+            if (lo >= hi) continue;
+            const int64_t i = lo + atomicAdd(a.tile_ctr + 16 * x, 1);
+            if (i < hi) return (int)i;
+        }
+        return (int)T;
+    };
+    if (tid == 0) *s_next = grab();
+    __syncthreads();
+    for (int64_t tile = *s_next; tile < a.n_tiles; tile = *s_next) {
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         // (addresses formed at use: nothing per tile stays live across the GEMMs)
         auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + opaque_lane(lane) * 4; };
@@ -1282,6 +1293,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
+        if (tid == 0) *s_next = grab();   // read after the barrier closing this iteration
         pre_publish_sync();
         publish_relu(x, tile, 2 * L.n_blocks);
         __syncthreads();
@@ -1350,6 +1362,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
         PT(gc, 4);
         PT_COUNT(gc, 6);
+        __syncthreads();   // s_next written; every wave leaves the head before the next tile
     }
 #ifdef PNR_PHASE_TIMING
     if (threadIdx.x == 0)
@@ -1686,8 +1699,9 @@ int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points) {
 }
 
 size_t mlp_xsum_bytes(int ns) {
-    (void)ns;  // x park + multi-view sum, one pair of 128 KB regions per resident workgroup
-    return sizeof(float) * (size_t)device_cu_count() * 2 * mlpk::COLS * mlpk::H;
+    (void)ns;  // x park + multi-view sum, one pair of 128 KB regions per resident workgroup,
+               // then the 8 per-XCD tile counters (512 B)
+    return sizeof(float) * (size_t)device_cu_count() * 2 * mlpk::COLS * mlpk::H + 512;
 }
 
 // Launch the fused model over n_points points (render mode if rays != nullptr).
@@ -1715,12 +1729,16 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.proj = proj;
     a.proj_stride = (int64_t)sc.n_obj * sc.n_views * sc.latent_h * sc.latent_w * mlpk::H;
     const int cus = device_cu_count();
+    if (a.n_tiles >= (1ll << 31)) return fail(PNR_ERR_UNSUPPORTED, "more than 2^31 point tiles in one launch");
+    a.tile_ctr = reinterpret_cast<int *>(xsum_ws + (size_t)cus * 2 * mlpk::COLS * mlpk::H);
+    if (hipMemsetAsync(a.tile_ctr, 0, 512, st) != hipSuccess) return fail(PNR_ERR_HIP, "point_mlp: hipMemsetAsync failed");
     const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
-    // PREC 3: split image P0 + P1, gather records, column maxima, exponents, PE table = 143,744 B
-    // else:   fp32 activations + staging ring + gather records + PE table          = 158,848 B
+    // PREC 3: split image P0 + P1, gather records, column maxima, exponents, PE table, next tile
+    //         = 143,760 B; else: fp32 activations + staging ring + gather records + PE table +
+    //         next tile = 158,864 B
     const size_t lds = d.precision == PNR_PREC_F16X3
-        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS + 32)
-        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8 + 32);
+        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS + 32 + 4)
+        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8 + 32 + 4);
 #define PNR_LAUNCH_MLP(P)                                                                              \
     do {                                                                                               \
         if (proj) hipLaunchKernelGGL((mlpk::k_point_mlp<P, true>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \
