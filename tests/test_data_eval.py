@@ -135,3 +135,65 @@ def test_eval_approx_end_to_end(tmp_path):
     gt = util.batched_index_select_nd(data["images"] * 0.5 + 0.5, dst).reshape(2, 3, 24, 24)
     p0 = evaluate.psnr_np(rgb.reshape(2, 24, 24, 3)[0].cpu().numpy(), gt.permute(0, 2, 3, 1)[0].numpy())
     assert abs(p0 - res["psnr"][0]) < 1e-5
+
+
+CLI_CONF = """
+model {
+    use_encoder = True
+    use_xyz = True
+    use_code = True
+    code { num_freqs = 6, freq_factor = 1.5, include_input = True }
+    use_viewdirs = True
+    use_code_viewdirs = False
+    mlp_coarse { type = resnet, n_blocks = 5, d_hidden = 512, combine_layer = 3, combine_type = average }
+    mlp_fine { type = resnet, n_blocks = 5, d_hidden = 512, combine_layer = 3, combine_type = average }
+    encoder { backbone = resnet34, pretrained = False, num_layers = 4 }
+}
+renderer {
+    n_coarse = 32
+    n_fine = 16
+    n_fine_depth = 8
+    depth_std = 0.01
+    white_bkgd = True
+}
+"""
+
+
+@pytest.mark.gpu
+def test_eval_and_video_scripts_end_to_end(tmp_path):
+    """scripts/eval_approx.py and scripts/gen_video.py as a user runs them: HOCON conf,
+    checkpoint through load_weights, SRN-layout dataset, on the HIP device."""
+    import os
+    import subprocess
+    import sys
+
+    from pnr import synth
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = _golden()
+    root = write_srn_dir(str(tmp_path), g)
+    (tmp_path / "exp.conf").write_text(CLI_CONF)
+    ck = tmp_path / "ck" / "synthnet"
+    ck.mkdir(parents=True)
+    sd = {k: v for k, v in synth.pixelnerf_state(2).items()}
+    # a full state dict: encoder weights from a fresh (random, pretrained=False) encoder
+    from pnr.models import make_model
+    from pnr.conf import parse_file
+
+    net = make_model(parse_file(str(tmp_path / "exp.conf"))["model"])
+    full = net.state_dict()
+    full.update(sd)
+    torch.save(full, str(ck / "pixel_nerf_latest"))
+    common = ["-c", str(tmp_path / "exp.conf"), "-D", root, "-n", "synthnet",
+              "--checkpoints_path", str(tmp_path / "ck"), "--split", "test"]
+    r = subprocess.run([sys.executable, os.path.join(repo, "scripts", "eval_approx.py"), *common, "-P", "1",
+                        "--batch_size", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "final psnr" in r.stdout
+    r = subprocess.run([sys.executable, os.path.join(repo, "scripts", "gen_video.py"), *common, "-P", "1",
+                        "-S", "1", "--num_views", "3", "--visual_path", str(tmp_path / "vis")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    frames = sorted(os.listdir(tmp_path / "vis" / "synthnet" / "videot0001_v001"))
+    assert frames == ["0000.png", "0001.png", "0002.png"]
+    assert (tmp_path / "vis" / "synthnet" / "videot0001_v001.gif").exists()
