@@ -812,15 +812,21 @@ struct GemmCtx {
 // contiguous 1 KB half of a corner's 2 KB row.  The stage aliases the GEMM input image, so
 // the first batch's loads are issued BEFORE the barrier that frees it (proj_load) and land
 // while the wave waits for its SIMD-mate's GEMM; blends and LDS writes come after.
-constexpr int PJ = 4;   // columns per batch
+#ifndef PNR_PJ
+#define PNR_PJ 4
+#endif
+constexpr int PJ = PNR_PJ;                // columns in the batch loaded before the barrier
+constexpr int PJ2 = COLS / WAVES - PJ;    // the rest, loaded after it
+template <int N>
 struct ProjRows {
-    f4 c[PJ][2][4];     // [column][channel half][corner]
-    f4 tw[PJ];          // bilinear weights nw, ne, sw, se
+    f4 c[N][2][4];      // [column][channel half][corner]
+    f4 tw[N];           // bilinear weights nw, ne, sw, se
 };
-__device__ __forceinline__ void proj_load(ProjRows &R, const float *__restrict__ pz, const float *gtab, int j0,
+template <int N>
+__device__ __forceinline__ void proj_load(ProjRows<N> &R, const float *__restrict__ pz, const float *gtab, int j0,
                                           int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < PJ; ++j) {
+    for (int j = 0; j < N; ++j) {
         const int cj = (COLS / WAVES) * wave + j0 + j;
         const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
         R.tw[j] = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
@@ -838,9 +844,10 @@ __device__ __forceinline__ void proj_load(ProjRows &R, const float *__restrict__
         }
     }
 }
-__device__ __forceinline__ void proj_blend_store(const ProjRows &R, float *stage, int j0, int wave, int lane) {
+template <int N>
+__device__ __forceinline__ void proj_blend_store(const ProjRows<N> &R, float *stage, int j0, int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < PJ; ++j) {
+    for (int j = 0; j < N; ++j) {
         const int cj = (COLS / WAVES) * wave + j0 + j;
         const f4 tw = R.tw[j];
 #pragma unroll
@@ -856,7 +863,7 @@ __device__ __forceinline__ void proj_blend_store(const ProjRows &R, float *stage
         }
     }
 }
-static_assert(2 * PJ == COLS / WAVES, "two batches cover a wave's columns");
+static_assert(PJ > 0 && PJ2 > 0, "two batches cover a wave's columns");
 static_assert(sizeof(float) * COLS * LDS_LD <= 2 * sizeof(_Float16) * PART_HALVES,
               "the fp32 stage fits in the split image it aliases");
 // x[r][c] += stage rows of this wave (column 16c + cl, rows 16 (RTW wave + r) + 4g ..)
@@ -1167,13 +1174,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     // the stage aliases the image the previous GEMM read; publish_relu's
                     // internal barrier orders the add_stage reads before the image writes
                     const float *pz = a.proj + blk * a.proj_stride;
-                    ProjRows rows;
+                    ProjRows<PJ> rows;
                     proj_load(rows, pz, gtab, 0, wave, lane);
                     __syncthreads();
                     PT(gc, 3);
                     proj_blend_store(rows, inbuf, 0, wave, lane);
-                    proj_load(rows, pz, gtab, PJ, wave, lane);
-                    proj_blend_store(rows, inbuf, PJ, wave, lane);
+                    ProjRows<PJ2> rows2;
+                    proj_load(rows2, pz, gtab, PJ, wave, lane);
+                    proj_blend_store(rows2, inbuf, PJ, wave, lane);
                     __syncthreads();
                     PT(gc, 1);
                     add_bias(x, bias + (1 + lz) * H, wave, lane, true);
