@@ -321,15 +321,15 @@ def pmc_traffic(kernel, render_pass):
     """Mean HBM bytes per launch of `kernel` in `render_pass` ("fine" / "coarse") from the
     newest committed PMC summary that has it (rocprofv3 counters cannot be read live from
     inside the process).  Returns (bytes, summary path) or (None, None)."""
+    import csv
     import glob
 
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")), reverse=True):
         vals = []
-        for line in open(path):
-            if line.startswith("#") or line.startswith("kernel,"):
-                continue
-            f = line.strip().split(",")
-            if f[0].endswith(kernel) and len(f) > 6 and f[6] == render_pass:
+        with open(path) as fh:
+            rows = [f for f in csv.reader(l for l in fh if not l.startswith("#") and not l.startswith("kernel,"))]
+        for f in rows:   # kernel names are quoted (they contain commas: k_point_mlp<3, true>)
+            if f and f[0].endswith(kernel) and len(f) > 6 and f[6] == render_pass:
                 vals.append(int(f[5]))
         if vals:
             return sum(vals) // len(vals), os.path.relpath(path, REPO)
