@@ -580,14 +580,28 @@ typedef unsigned u2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f4 mfma_h(h8 a, h8 b, f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
-// 4 values * s -> packed fp16 parts (2 dwords each): v_cvt_pk_f16_f32 (RNE), back, subtract
+// fp16 residuals of a pair: f16(x - f32(h.lo)), f16(y - f32(h.hi)) by v_fma_mix{lo,hi}_f16
+// (the fp16 operand widened in the instruction, one rounding of the exact difference: the
+// same bits as subtracting in fp32 and converting, in 2 instructions instead of 5)
+__device__ __forceinline__ unsigned resid_pk(unsigned h, float x, float y) {
+#ifdef PNR_NO_FMA_MIX
+    const h2 hh = __builtin_bit_cast(h2, h);
+    const f2 r = f2{x, y} - __builtin_convertvector(hh, f2);
+    return __builtin_bit_cast(unsigned, __builtin_convertvector(r, h2));
+#else
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h), "v"(x));
+    asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(d) : "v"(h), "v"(y));
+    return d;
+#endif
+}
+// 4 values * s -> packed fp16 parts (2 dwords each): v_cvt_pk_f16_f32 (RNE), residuals
 __device__ __forceinline__ void split_f16x4(const f4 &v, float s, u2 &p0, u2 &p1) {
     const f2 a = {v.x * s, v.y * s}, b = {v.z * s, v.w * s};
-    const h2 a0 = __builtin_convertvector(a, h2), b0 = __builtin_convertvector(b, h2);
-    const f2 ar = a - __builtin_convertvector(a0, f2), br = b - __builtin_convertvector(b0, f2);
-    const h2 a1 = __builtin_convertvector(ar, h2), b1 = __builtin_convertvector(br, h2);
-    p0 = u2{__builtin_bit_cast(unsigned, a0), __builtin_bit_cast(unsigned, b0)};
-    p1 = u2{__builtin_bit_cast(unsigned, a1), __builtin_bit_cast(unsigned, b1)};
+    const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_convertvector(a, h2));
+    const unsigned b0 = __builtin_bit_cast(unsigned, __builtin_convertvector(b, h2));
+    p0 = u2{a0, b0};
+    p1 = u2{resid_pk(a0, a.x, a.y), resid_pk(b0, b.x, b.y)};
 }
 
 // LDS image of the GEMM input in PREC 3: each activation column c scaled by 2^e_c and
