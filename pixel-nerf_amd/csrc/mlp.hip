@@ -623,14 +623,17 @@ __device__ __forceinline__ int swz(int col, int k) {
 // flight when the accumulators are handed back.
 //   pb0 / pb1: P0 / P1 at (column cl, k 8g) of column tile 0
 #ifndef PNR_H_DIST
-#define PNR_H_DIST 3
+#define PNR_H_DIST 4
 #endif
-constexpr int H_DIST = PNR_H_DIST;               // f16 weight prefetch distance (row tiles)
-constexpr int H_RING = H_DIST < RTW ? RTW : 2 * RTW;   // register ring slots
-static_assert(H_DIST < H_RING && H_RING % RTW == 0, "ring");
-template <int NKS>
+constexpr int H_DIST = PNR_H_DIST;   // f16 weight prefetch distance (row tiles) of the forward:
+                                     // 4 measured 1.7 % faster than 3 (5, 6 slower)
+constexpr int H_DIST_3 = 3;          // k_mlp_bwd and the gather-path forward (training):
+                                     // 4 spills there
+template <int NKS, int DIST = H_DIST>
 __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
                                          const _Float16 *pb1) {
+    constexpr int H_RING = DIST < RTW ? RTW : 2 * RTW;   // register ring slots
+    static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
     static_assert(NKS % U == 0, "k-steps");
     h8 ra[H_RING][2];
@@ -644,7 +647,7 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
         ra[slot][1] = *reinterpret_cast<const h8 *>(src + 256);
     };
 #pragma unroll
-    for (int t = 0; t < H_DIST; ++t) loadA(t, t / RTW, t % RTW);
+    for (int t = 0; t < DIST; ++t) loadA(t, t / RTW, t % RTW);
     // one k-step; ph = ks % U (static), tail = this is one of the last U k-steps
     auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
         constexpr int ph = decltype(ph_tag)::value;
@@ -657,7 +660,7 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
         }
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
-            const int tn = ph * RTW + r + H_DIST;          // prefetch target, relative to the iteration
+            const int tn = ph * RTW + r + DIST;            // prefetch target, relative to the iteration
             if (!tail || tn < U * RTW) loadA(tn % H_RING, ks - ph + tn / RTW, tn % RTW);
             __builtin_amdgcn_sched_barrier(0);
             const h8 *a = ra[(ph * RTW + r) % H_RING];
@@ -897,7 +900,7 @@ __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, 
 }
 
 // hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index)
-template <int PREC, int NK>
+template <int PREC, int NK, int DIST = H_DIST>
 __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx) {
     PT(g, 3);
     PT_COUNT(g, 5);
@@ -919,7 +922,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
-        gemm_f16<NK / 2>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
+        gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -933,6 +936,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
 // PZ: lin_z from the projected latent (gather_proj) instead of the latent gather + GEMM
 template <int PREC, bool PZ>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
+    constexpr int KD = PZ ? H_DIST : H_DIST_3;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
     const int tid = threadIdx.x;
@@ -1180,7 +1184,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, lane, false);
-            layer_gemm<PREC, NKB_IN>(x, a.packed + L.off_lin_in, gc, 0);
+            layer_gemm<PREC, NKB_IN, KD>(x, a.packed + L.off_lin_in, gc, 0);
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
@@ -1254,20 +1258,20 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 __syncthreads();
                 PT(gc, 1);
                 add_bias(x, bias + (1 + lz) * H, wave, lane, true);
-                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
+                layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 pre_publish_sync();
                 }
                 publish_relu(x, tile, blk);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, lane, false);
-                layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
+                layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
                 pre_publish_sync();
                 publish_relu(h, tile, L.n_blocks + blk);
                 __syncthreads();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
                 add_bias(x, bias + (3 + lz) * H, wave, lane, true);
-                layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz);
+                layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -1306,13 +1310,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, lane, false);
-            layer_gemm<PREC, NKB>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
+            layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
             pre_publish_sync();
             publish_relu(h, tile, L.n_blocks + blk);
             __syncthreads();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
             add_bias(x, bias + (2 + l0) * H, wave, lane, true);
-            layer_gemm<PREC, NKB>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
+            layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = grab();   // read after the barrier closing this iteration
@@ -1536,13 +1540,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
             const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
             zero(h);
             load_mask(mk, mask_slot(nb + b), tile, P, wave, lane);   // lands during the GEMM
-            layer_gemm<3, NKB>(h, layer(l1), gc, 1 + l1);
+            layer_gemm<3, NKB, H_DIST_3>(h, layer(l1), gc, 1 + l1);
             relu_mask(h, mk, tile, P, lane);
             store_rows(h, dy_slot(b), tile, P, wave, lane);
             publish(h);
             zero(h);
             load_mask(mk, mask_slot(b), tile, P, wave, lane);
-            layer_gemm<3, NKB>(h, layer(l0), gc, 1 + l0);
+            layer_gemm<3, NKB, H_DIST_3>(h, layer(l0), gc, 1 + l0);
             relu_mask(h, mk, tile, P, lane);
 #pragma unroll
             for (int r = 0; r < RTW; ++r)
@@ -1554,7 +1558,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                 published = true;
                 const int lz = layer_index(b, 0, L.n_linz);
                 zero(h);
-                layer_gemm<3, NKB>(h, layer(lz), gc, 1 + lz);
+                layer_gemm<3, NKB, H_DIST_3>(h, layer(lz), gc, 1 + lz);
                 const bool first = b == L.n_linz - 1;
 #pragma unroll
                 for (int c = 0; c < CT; ++c) {
