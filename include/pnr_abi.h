@@ -256,18 +256,21 @@ int pnr_latent_channels_last(const float *const *maps, const int32_t *channels,
                              pnr_stream_t stream);
 
 /* ---- training (autograd over the ray march) ------------ */
-/* Floats of the activation save of pnr_render_points for n_points points:
- * per point features (64) | z (512) | relu(x) into fc_0 of each block (512 each) |
- * relu(h) of each block (512 each) | relu(x) into lin_out (512), each region [point][width],
- * then the relu sign masks of the 2 n_blocks + 1 relu regions (same order), each
- * [point][64 bytes], [activation n > 0] of n = 64 w + 16 r + 4 g + e (w, r, g, e =
- * 0..7, 0..3, 0..3, 0..3) at bit 4 (r & 1) + e of byte 8 w + 2 g + (r >> 1). */
+/* Floats of the activation save of pnr_render_points for n_points rows; call it with
+ * n_points = n_rays * k * n_views.  Regions, each [row][width] with R = n_rays * k *
+ * n_views rows: features (64) | z (512) | relu(x) into fc_0 of each block (512 each) |
+ * relu(h) of each block (512 each) | relu(x) into lin_out (512), then the relu sign masks
+ * of the 2 n_blocks + 1 relu regions (same order), each [row][64 bytes], [activation n > 0]
+ * of n = 64 w + 16 r + 4 g + e (w, r, g, e = 0..7, 0..3, 0..3, 0..3) at bit 4 (r & 1) + e
+ * of byte 8 w + 2 g + (r >> 1).  Row v * (n_rays * k) + p holds (source view v, point p)
+ * for the per-view stages (features, z, the blocks before combine_layer); the blocks from
+ * combine_layer on and lin_out use rows p < n_rays * k (the view mean). */
 size_t pnr_point_save_floats(const pnr_mlp_desc *desc, int64_t n_points);
 
 /* Replaces: the model call of NeRFRenderer.composite (nerf.py:182-216) under autograd:
  * PixelNeRFNet.forward at the points o + z d of every ray (z (n_rays, k)), writing
  * out (n_rays * k, 4) and, when `save` is not NULL, the activations the backward needs
- * (n_views must be 1).  Workspace as pnr_point_query. */
+ * (pnr_point_save_floats(desc, n_rays * k * n_views) floats).  Workspace as pnr_point_query. */
 int pnr_render_points(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
                       const pnr_rays *rays, const float *z, int32_t k, float *out, float *save,
                       void *workspace, size_t workspace_bytes, pnr_stream_t stream);
@@ -280,10 +283,11 @@ int pnr_composite_backward(const float *z, const float *raw, const float *rays, 
                            const float *d_weights, float *d_raw, float *d_z, pnr_stream_t stream);
 
 /* Replaces: autograd of the input stage of PixelNeRFNet.forward (models.py:156-221,
- * code.py:30-42, encoder.py:80-109) for n_views == 1.  d_feat (n_rays * k, 64): gradient of
- * the lin_in input; d_zlat (n_rays * k, 512): gradient of the sampled latent feature.
- * Accumulates d_latent (channels-last, like scene->latent; may be NULL) and writes d_z
- * (n_rays * k, may be NULL) = dL / d z_sample.  `packed` supplies the PE buffers. */
+ * code.py:30-42, encoder.py:80-109).  d_feat (n_views * n_rays * k, 64): gradient of the
+ * lin_in input; d_zlat (n_views * n_rays * k, 512): gradient of the sampled latent feature,
+ * rows as the activation save (view-major).  Accumulates d_latent (channels-last, like
+ * scene->latent; may be NULL) and writes d_z (n_rays * k, may be NULL) = dL / d z_sample,
+ * summed over the views in view order.  `packed` supplies the PE buffers. */
 int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
                               const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
                               const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream);

@@ -36,7 +36,7 @@ int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, con
                      int, int, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
                          const float *, const float *, float *, float *, hipStream_t);
-int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, const float *, const float *,
+int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, int, const float *, const float *,
                          int, int, float, float, const float *, int, const float *, const float *, float *,
                          float *, hipStream_t);
 int launch_point_mlp(const pnr_scene &, const pnr_mlp_desc &, const void *, const float *,
@@ -190,8 +190,6 @@ int pnr_render_points(const pnr_scene *scene, const pnr_mlp_desc *desc, const vo
     if ((rc = check_desc_for_scene(desc, scene))) return rc;
     if ((rc = check_rays_z(scene, rays, z, k))) return rc;
     if (!packed || !out) return fail(PNR_ERR_INVALID, "pnr_render_points: NULL pointer");
-    if (save && scene->n_views != 1)
-        return fail(PNR_ERR_UNSUPPORTED, "activation save (training) implements n_views == 1");
     const int64_t n_points = rays->n_rays * k;
     if (n_points == 0) return PNR_OK;
     const size_t need = pnr_point_query_workspace_bytes(scene, n_points);
@@ -221,10 +219,9 @@ int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, 
     if (rc) return rc;
     if ((rc = check_desc_for_scene(desc, scene))) return rc;
     if ((rc = check_rays_z(scene, rays, z, k))) return rc;
-    if (scene->n_views != 1) return fail(PNR_ERR_UNSUPPORTED, "input backward implements n_views == 1");
     if (scene->latent_c != 512) return fail(PNR_ERR_UNSUPPORTED, "input backward: latent_c == 512");
     if (!packed || !d_feat || !d_zlat) return fail(PNR_ERR_INVALID, "pnr_points_input_backward: NULL");
-    return launch_points_in_bwd(rays->rays, z, k, rays->rays_per_obj, rays->n_rays * k, scene->cams,
+    return launch_points_in_bwd(rays->rays, z, k, rays->rays_per_obj, rays->n_rays * k, scene->n_views, scene->cams,
                                 scene->latent, scene->latent_h, scene->latent_w, scene->image_w,
                                 scene->image_h, static_cast<const float *>(packed), desc->pe_n, d_feat,
                                 d_zlat, d_latent, d_z, (hipStream_t)stream);

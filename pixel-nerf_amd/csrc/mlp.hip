@@ -983,10 +983,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 
     // relu(acc) -> the next GEMM's input image (callers barrier before and after)
     // activation save slots (training forward)
-    const int64_t P = a.n_points;
-    float *sv_f = a.save, *sv_z = a.save ? a.save + P * 64 : nullptr;
-    auto sv_slot = [&](int i) { return sv_z + P * H * (1 + i); };   // i: block b -> x_in, nb + b -> h, 2nb -> x_f
-    uint32_t *sv_mask = a.save ? reinterpret_cast<uint32_t *>(a.save + save_mask_offset(L.n_blocks, P)) : nullptr;
+    // Every region has PS = n_points * n_views rows: row v P + p holds (view v, point p) of
+    // the per-view stages (features, z, the blocks before the combine layer), row p the
+    // per-point stages after it (their other rows are unused).
+    const int64_t P = a.n_points, PS = P * a.ns;
+    float *sv_f = a.save, *sv_z = a.save ? a.save + PS * 64 : nullptr;
+    auto sv_slot = [&](int i) { return sv_z + PS * H * (1 + i); };   // i: block b -> x_in, nb + b -> h, 2nb -> x_f
+    uint32_t *sv_mask = a.save ? reinterpret_cast<uint32_t *>(a.save + save_mask_offset(L.n_blocks, PS)) : nullptr;
     // Barrier between a GEMM that reads the input image and the publish that rewrites it.
     // PREC 3's publish writes only its column maxima before its own internal barrier, and
     // the image after it, so there the barrier is redundant and waves that finish their GEMM
@@ -997,10 +1000,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
             __syncthreads();
     };
-    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx) {
+    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (a.save) {
-            save_relu(acc, sv_slot(save_idx), tile, P, wave, lane);
-            save_mask(acc, sv_mask + P * 16 * save_idx, tile, P, wave, lane);
+            save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
+            save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
         }
 #ifdef PNR_GEMM_ONLY
         {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
@@ -1122,7 +1125,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 if (a.save && p_raw < a.n_points) {
 #pragma unroll
                     for (int i = 0; i < FPT / 4; ++i)
-                        *reinterpret_cast<f4 *>(sv_f + p_raw * 64 + FPT * qt + 4 * i) =
+                        *reinterpret_cast<f4 *>(sv_f + (v * P + p_raw) * 64 + FPT * qt + 4 * i) =
                             f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]};
                 }
                 if constexpr (PREC == 3) {
@@ -1238,7 +1241,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                         if constexpr (PREC == 3) zh[half] = zz;
                         else *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
                         if (a.save && blk == 0 && tile * COLS + cj < P)
-                            *reinterpret_cast<f4 *>(sv_z + (tile * COLS + cj) * H + ch) = zz;
+                            *reinterpret_cast<f4 *>(sv_z + (v * P + tile * COLS + cj) * H + ch) = zz;
                     }
                     if constexpr (PREC == 3) {
                         // column max over the wave (all 512 channels), scale, split
@@ -1261,13 +1264,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 pre_publish_sync();
                 }
-                publish_relu(x, tile, blk);
+                publish_relu(x, tile, blk, v * P);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 __syncthreads();
                 add_bias(h, bias + (2 + lz) * H, wave, lane, false);
                 layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
                 pre_publish_sync();
-                publish_relu(h, tile, L.n_blocks + blk);
+                publish_relu(h, tile, L.n_blocks + blk, v * P);
                 __syncthreads();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
                 add_bias(x, bias + (3 + lz) * H, wave, lane, true);
@@ -1306,13 +1309,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             pre_publish_sync();
-            publish_relu(x, tile, blk);
+            publish_relu(x, tile, blk, 0);
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
             __syncthreads();
             add_bias(h, bias + (1 + l0) * H, wave, lane, false);
             layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
             pre_publish_sync();
-            publish_relu(h, tile, L.n_blocks + blk);
+            publish_relu(h, tile, L.n_blocks + blk, 0);
             __syncthreads();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
             add_bias(x, bias + (2 + l0) * H, wave, lane, true);
@@ -1321,7 +1324,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = grab();   // read after the barrier closing this iteration
         pre_publish_sync();
-        publish_relu(x, tile, 2 * L.n_blocks);
+        publish_relu(x, tile, 2 * L.n_blocks, 0);
         __syncthreads();
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY

@@ -139,7 +139,7 @@ struct PointGeo {
 
 __device__ __forceinline__ PointGeo point_geo(const float *__restrict__ rays, const float *__restrict__ zs, int K,
                                               int64_t rays_per_obj, const float *__restrict__ cams, int hl, int wl,
-                                              float img_w, float img_h, int64_t p) {
+                                              float img_w, float img_h, int64_t p, int ns, int v) {
     PointGeo G;
     const int64_t b = p / K;
     const float *ray = rays + b * 8;
@@ -147,8 +147,8 @@ __device__ __forceinline__ PointGeo point_geo(const float *__restrict__ rays, co
     const float px = add_rn(ray[0], mul_rn(zz, ray[3]));
     const float py = add_rn(ray[1], mul_rn(zz, ray[4]));
     const float pz = add_rn(ray[2], mul_rn(zz, ray[5]));
-    const int64_t obj = b / rays_per_obj;
-    const float *cam = cams + obj * 16;
+    const int64_t cv = (b / rays_per_obj) * ns + v;   // camera / latent of (object, view v)
+    const float *cam = cams + cv * 16;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         G.xr[i] = add_rn(add_rn(mul_rn(cam[3 * i], px), mul_rn(cam[3 * i + 1], py)), mul_rn(cam[3 * i + 2], pz));
@@ -170,7 +170,7 @@ __device__ __forceinline__ PointGeo point_geo(const float *__restrict__ rays, co
     const int x0 = (int)floorf(G.ix), y0 = (int)floorf(G.iy);
     G.inx1 = x0 + 1 < wl;
     G.iny1 = y0 + 1 < hl;
-    const int64_t base = obj * (int64_t)hl * wl * 512;
+    const int64_t base = cv * (int64_t)hl * wl * 512;
     const int x1 = G.inx1 ? x0 + 1 : x0, y1 = G.iny1 ? y0 + 1 : y0;
     G.o00 = base + ((int64_t)y0 * wl + x0) * 512;
     G.o01 = base + ((int64_t)y0 * wl + x1) * 512;
@@ -181,114 +181,119 @@ __device__ __forceinline__ PointGeo point_geo(const float *__restrict__ rays, co
 
 __global__ __launch_bounds__(256) void k_points_in_bwd(
     const float *__restrict__ rays, const float *__restrict__ zs, int K, int64_t rays_per_obj,
-    int64_t n_points, const float *__restrict__ cams, const float *__restrict__ latent, int hl, int wl,
+    int64_t n_points, int ns, const float *__restrict__ cams, const float *__restrict__ latent, int hl, int wl,
     float img_w, float img_h, const float *__restrict__ pe, int pe_n, const float *__restrict__ d_feat,
     const float *__restrict__ d_zlat, float *__restrict__ d_latent, float *__restrict__ d_z) {
     const int lane = threadIdx.x & 63;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RUN;
     if (p0 >= n_points) return;
     const int n_run = n_points - p0 < RUN ? (int)(n_points - p0) : RUN;
-    // current cell's corner gradients: [corner][half] x 4 channels (lane * 4 + 256 half)
-    f4 acc[4][2];
-    int64_t cur = -1;
-    bool cur_x1 = false, cur_y1 = false;
-    int64_t c01 = 0, c10 = 0, c11 = 0;
-    auto flush = [&]() {
-        if (cur < 0 || !d_latent) return;
+    // d_feat / d_zlat rows v n_points + p: (view v, point p); d_z sums the views in order
+    float dz_sum = 0.f;   // lane j: point p0 + j
+    for (int v = 0; v < ns; ++v) {
+        // current cell's corner gradients: [corner][half] x 4 channels (lane * 4 + 256 half)
+        f4 acc[4][2];
+        int64_t cur = -1;
+        bool cur_x1 = false, cur_y1 = false;
+        int64_t c01 = 0, c10 = 0, c11 = 0;
+        auto flush = [&]() {
+            if (cur < 0 || !d_latent) return;
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int ch = half * 256 + lane * 4;
+            for (int half = 0; half < 2; ++half) {
+                const int ch = half * 256 + lane * 4;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                atomicAdd(d_latent + cur + ch + q, acc[0][half][q]);
-                if (cur_x1) atomicAdd(d_latent + c01 + ch + q, acc[1][half][q]);
-                if (cur_y1) atomicAdd(d_latent + c10 + ch + q, acc[2][half][q]);
-                if (cur_x1 && cur_y1) atomicAdd(d_latent + c11 + ch + q, acc[3][half][q]);
+                for (int q = 0; q < 4; ++q) {
+                    atomicAdd(d_latent + cur + ch + q, acc[0][half][q]);
+                    if (cur_x1) atomicAdd(d_latent + c01 + ch + q, acc[1][half][q]);
+                    if (cur_y1) atomicAdd(d_latent + c10 + ch + q, acc[2][half][q]);
+                    if (cur_x1 && cur_y1) atomicAdd(d_latent + c11 + ch + q, acc[3][half][q]);
+                }
+            }
+        };
+        float dix_run = 0.f, diy_run = 0.f;   // lane j: point j's d ix / d iy (wave sums)
+        for (int j = 0; j < n_run; ++j) {
+            const int64_t p = p0 + j;
+            const PointGeo G = point_geo(rays, zs, K, rays_per_obj, cams, hl, wl, img_w, img_h, p, ns, v);
+            const float we = sub_rn(G.ix, floorf(G.ix)), wn = sub_rn(G.iy, floorf(G.iy));
+            const float wnw = mul_rn(sub_rn(1.f, wn), sub_rn(1.f, we)), wne = mul_rn(sub_rn(1.f, wn), we);
+            const float wsw = mul_rn(wn, sub_rn(1.f, we)), wse = mul_rn(wn, we);
+            if (G.o00 != cur) {   // wave-uniform
+                flush();
+                cur = G.o00;
+                c01 = G.o01; c10 = G.o10; c11 = G.o11;
+                cur_x1 = G.inx1; cur_y1 = G.iny1;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc[c][0] = acc[c][1] = f4{0.f, 0.f, 0.f, 0.f};
+            }
+            float dwe = 0.f, dwn = 0.f;
+            const float *gz = d_zlat + (v * n_points + p) * 512;
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const int ch = half * 256 + lane * 4;
+                const f4 gv = *reinterpret_cast<const f4 *>(gz + ch);
+                const f4 l00 = *reinterpret_cast<const f4 *>(latent + G.o00 + ch);
+                f4 l01 = *reinterpret_cast<const f4 *>(latent + G.o01 + ch);
+                f4 l10 = *reinterpret_cast<const f4 *>(latent + G.o10 + ch);
+                f4 l11 = *reinterpret_cast<const f4 *>(latent + G.o11 + ch);
+                if (!G.inx1) { l01 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l01; }
+                if (!G.iny1) { l10 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l10; }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    dwe += gv[q] * ((1.f - wn) * (l01[q] - l00[q]) + wn * (l11[q] - l10[q]));
+                    dwn += gv[q] * ((1.f - we) * (l10[q] - l00[q]) + we * (l11[q] - l01[q]));
+                }
+                acc[0][half] += wnw * gv;
+                acc[1][half] += wne * gv;
+                acc[2][half] += wsw * gv;
+                acc[3][half] += wse * gv;
+            }
+            if (d_z) {
+                dwe = wave_sum_dpp(dwe);
+                dwn = wave_sum_dpp(dwn);
+                if (lane == j) { dix_run = dwe; diy_run = dwn; }
             }
         }
-    };
-    float dix_run = 0.f, diy_run = 0.f;   // lane j: point j's d ix / d iy (wave sums)
-    for (int j = 0; j < n_run; ++j) {
-        const int64_t p = p0 + j;
-        const PointGeo G = point_geo(rays, zs, K, rays_per_obj, cams, hl, wl, img_w, img_h, p);
-        const float we = sub_rn(G.ix, floorf(G.ix)), wn = sub_rn(G.iy, floorf(G.iy));
-        const float wnw = mul_rn(sub_rn(1.f, wn), sub_rn(1.f, we)), wne = mul_rn(sub_rn(1.f, wn), we);
-        const float wsw = mul_rn(wn, sub_rn(1.f, we)), wse = mul_rn(wn, we);
-        if (G.o00 != cur) {   // wave-uniform
-            flush();
-            cur = G.o00;
-            c01 = G.o01; c10 = G.o10; c11 = G.o11;
-            cur_x1 = G.inx1; cur_y1 = G.iny1;
+        flush();
+        if (!d_z || lane >= n_run) continue;
+        // lane j: the dL/dz chain of point p0 + j through view v
+        const int64_t p = p0 + lane;
+        const PointGeo G = point_geo(rays, zs, K, rays_per_obj, cams, hl, wl, img_w, img_h, p, ns, v);
+        const float *ray = rays + (p / K) * 8;
+        const float *cam = cams + (((p / K) / rays_per_obj) * ns + v) * 16;
+        const float fx = cam[12], fy = cam[13];
+        const float wlf = (float)wl, hlf = (float)hl;
+        const float sx = __fdiv_rn(mul_rn(__fdiv_rn(wlf, sub_rn(wlf, 1.f)), 2.f), img_w);
+        const float sy = __fdiv_rn(mul_rn(__fdiv_rn(hlf, sub_rn(hlf, 1.f)), 2.f), img_h);
+        const float hx = mul_rn(sub_rn(wlf, 1.f), 0.5f), hy = mul_rn(sub_rn(hlf, 1.f), 0.5f);
+        // torch clip_coordinates_set_grad: borders count as out of bounds (NaN -> 0)
+        const float gclip_x = (G.ixu > 0.f && G.ixu < wlf - 1.f) ? 1.f : 0.f;
+        const float gclip_y = (G.iyu > 0.f && G.iyu < hlf - 1.f) ? 1.f : 0.f;
+        // projection chain: ix = (gx + 1) hx, gx = u sx - 1, u = -(xc0 / xc2) fx + cx
+        const float du = dix_run * gclip_x * hx * sx, dv = diy_run * gclip_y * hy * sy;
+        const float inv = 1.f / G.xc[2];
+        float dxc[3];
+        dxc[0] = -du * fx * inv;
+        dxc[1] = -dv * fy * inv;
+        dxc[2] = (du * fx * G.xc[0] + dv * fy * G.xc[1]) * inv * inv;
+        // features: x_rot (3) then PE sin(phase_q + x_rot_j freq_q) at 3 + 3q + j
+        const float *df = d_feat + (v * n_points + p) * 64;
+        float dxr[3] = {df[0] + dxc[0], df[1] + dxc[1], df[2] + dxc[2]};
+        for (int q = 0; q < pe_n; ++q) {
+            const float f = pe[q], ph = pe[16 + q];
 #pragma unroll
-            for (int c = 0; c < 4; ++c) acc[c][0] = acc[c][1] = f4{0.f, 0.f, 0.f, 0.f};
+            for (int jj = 0; jj < 3; ++jj)
+                dxr[jj] += df[3 + 3 * q + jj] * cosf(add_rn(ph, mul_rn(G.xr[jj], f))) * f;
         }
-        float dwe = 0.f, dwn = 0.f;
-        const float *gz = d_zlat + p * 512;
+        // x_rot = R x, x = o + z d
+        float dzs = 0.f;
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const int ch = half * 256 + lane * 4;
-            const f4 gv = *reinterpret_cast<const f4 *>(gz + ch);
-            const f4 l00 = *reinterpret_cast<const f4 *>(latent + G.o00 + ch);
-            f4 l01 = *reinterpret_cast<const f4 *>(latent + G.o01 + ch);
-            f4 l10 = *reinterpret_cast<const f4 *>(latent + G.o10 + ch);
-            f4 l11 = *reinterpret_cast<const f4 *>(latent + G.o11 + ch);
-            if (!G.inx1) { l01 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l01; }
-            if (!G.iny1) { l10 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l10; }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                dwe += gv[q] * ((1.f - wn) * (l01[q] - l00[q]) + wn * (l11[q] - l10[q]));
-                dwn += gv[q] * ((1.f - we) * (l10[q] - l00[q]) + we * (l11[q] - l01[q]));
-            }
-            acc[0][half] += wnw * gv;
-            acc[1][half] += wne * gv;
-            acc[2][half] += wsw * gv;
-            acc[3][half] += wse * gv;
+        for (int i = 0; i < 3; ++i) {
+            const float dxw = cam[i] * dxr[0] + cam[3 + i] * dxr[1] + cam[6 + i] * dxr[2];
+            dzs += dxw * ray[3 + i];
         }
-        if (d_z) {
-            dwe = wave_sum_dpp(dwe);
-            dwn = wave_sum_dpp(dwn);
-            if (lane == j) { dix_run = dwe; diy_run = dwn; }
-        }
+        dz_sum = v == 0 ? dzs : dz_sum + dzs;
     }
-    flush();
-    if (!d_z || lane >= n_run) return;
-    // lane j: the dL/dz chain of point p0 + j
-    const int64_t p = p0 + lane;
-    const PointGeo G = point_geo(rays, zs, K, rays_per_obj, cams, hl, wl, img_w, img_h, p);
-    const float *ray = rays + (p / K) * 8;
-    const float *cam = cams + ((p / K) / rays_per_obj) * 16;
-    const float fx = cam[12], fy = cam[13];
-    const float wlf = (float)wl, hlf = (float)hl;
-    const float sx = __fdiv_rn(mul_rn(__fdiv_rn(wlf, sub_rn(wlf, 1.f)), 2.f), img_w);
-    const float sy = __fdiv_rn(mul_rn(__fdiv_rn(hlf, sub_rn(hlf, 1.f)), 2.f), img_h);
-    const float hx = mul_rn(sub_rn(wlf, 1.f), 0.5f), hy = mul_rn(sub_rn(hlf, 1.f), 0.5f);
-    // torch clip_coordinates_set_grad: borders count as out of bounds (NaN -> 0)
-    const float gclip_x = (G.ixu > 0.f && G.ixu < wlf - 1.f) ? 1.f : 0.f;
-    const float gclip_y = (G.iyu > 0.f && G.iyu < hlf - 1.f) ? 1.f : 0.f;
-    // projection chain: ix = (gx + 1) hx, gx = u sx - 1, u = -(xc0 / xc2) fx + cx
-    const float du = dix_run * gclip_x * hx * sx, dv = diy_run * gclip_y * hy * sy;
-    const float inv = 1.f / G.xc[2];
-    float dxc[3];
-    dxc[0] = -du * fx * inv;
-    dxc[1] = -dv * fy * inv;
-    dxc[2] = (du * fx * G.xc[0] + dv * fy * G.xc[1]) * inv * inv;
-    // features: x_rot (3) then PE sin(phase_q + x_rot_j freq_q) at 3 + 3q + j
-    const float *df = d_feat + p * 64;
-    float dxr[3] = {df[0] + dxc[0], df[1] + dxc[1], df[2] + dxc[2]};
-    for (int q = 0; q < pe_n; ++q) {
-        const float f = pe[q], ph = pe[16 + q];
-#pragma unroll
-        for (int jj = 0; jj < 3; ++jj)
-            dxr[jj] += df[3 + 3 * q + jj] * cosf(add_rn(ph, mul_rn(G.xr[jj], f))) * f;
-    }
-    // x_rot = R x, x = o + z d
-    float dzs = 0.f;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        const float dxw = cam[i] * dxr[0] + cam[3 + i] * dxr[1] + cam[6 + i] * dxr[2];
-        dzs += dxw * ray[3 + i];
-    }
-    d_z[p] = dzs;
+    if (d_z && lane < n_run) d_z[p0 + lane] = dz_sum;
 }
 
 // ---------------------------------------------------------------------------
@@ -306,13 +311,13 @@ int launch_composite_bwd(const float *z, const float *raw, const float *rays, in
 }
 
 int launch_points_in_bwd(const float *rays, const float *zs, int K, int64_t rays_per_obj, int64_t n_points,
-                         const float *cams, const float *latent, int hl, int wl, float img_w, float img_h,
+                         int ns, const float *cams, const float *latent, int hl, int wl, float img_w, float img_h,
                          const float *pe, int pe_n, const float *d_feat, const float *d_zlat,
                          float *d_latent, float *d_z, hipStream_t st) {
     if (n_points == 0) return PNR_OK;
     const int64_t waves = (n_points + RUN - 1) / RUN;
     hipLaunchKernelGGL(k_points_in_bwd, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, rays, zs, K,
-                       rays_per_obj, n_points, cams, latent, hl, wl, img_w, img_h, pe, pe_n, d_feat, d_zlat,
+                       rays_per_obj, n_points, ns, cams, latent, hl, wl, img_w, img_h, pe, pe_n, d_feat, d_zlat,
                        d_latent, d_z);
     return launch_ok("points_in_bwd") ? PNR_OK : PNR_ERR_HIP;
 }

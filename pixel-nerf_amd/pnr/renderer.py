@@ -162,8 +162,6 @@ class NeRFRenderer(torch.nn.Module):
         r = net.hip_unsupported_reason()
         if r:
             raise NotImplementedError("pnr: " + r)
-        if net.num_views_per_obj != 1:
-            raise NotImplementedError("pnr: the training path implements one source view per object")
         if rays.device.type != "cuda":
             raise ValueError("pnr: rays must be on the HIP device")
         kc = self.n_coarse

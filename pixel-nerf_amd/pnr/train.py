@@ -22,7 +22,12 @@ The renderer wires them as the reference's autograd graph does:
 * the fine depths are sorted with ``torch.sort`` (nerf.py:295), so the gradient follows
   the permutation.
 
-Only n_views == 1 is implemented (the SRN training configuration).
+Several source views per object (train.py -V, the DTU setting) are supported: the
+activation save holds one row per (view, point) for the stages before combine_layer, the
+backward sends dL/d(view mean) / NS to every view there (util.combine_interleaved,
+util.py:461-471) and the input-stage backward scatters into each view's latent.  The fused
+f16x3 backward chain (``pnr_mlp_backward``) covers one view; with more, the ResnetFC
+backward runs as per-layer GEMMs (``mlp_backward``) for either forward arithmetic.
 """
 import torch
 
@@ -36,30 +41,35 @@ def mlp_params(mlp):
     return list(mlp.parameters())
 
 
-def _save_views(save, P, n_blocks, H=512):
-    """Slices of the pnr_render_points activation save (include/pnr_abi.h)."""
-    feat = save[: P * 64].view(P, 64)
-    base = P * 64
-    z = save[base: base + P * H].view(P, H)
+def _save_views(save, P, n_blocks, H=512, ns=1):
+    """Slices of the pnr_render_points activation save (include/pnr_abi.h): every region
+    has R = ns * P rows, row v P + p = (view v, point p); ``slot(i, rows)`` takes the first
+    ``rows`` rows of relu region i (P for the per-point stages after combine_layer)."""
+    R = ns * P
+    feat = save[: R * 64].view(R, 64)
+    base = R * 64
+    z = save[base: base + R * H].view(R, H)
 
-    def slot(i):
-        o = base + P * H * (1 + i)
-        return save[o: o + P * H].view(P, H)
+    def slot(i, rows=R):
+        o = base + R * H * (1 + i)
+        return save[o: o + rows * H].view(rows, H)
 
     return feat, z, slot
 
 
-def mlp_backward(mlp, save, d_o, P):
-    """ResnetFC backward (resnetfc.py:132-184, n_views == 1) given dL/d(pre-head output)
-    ``d_o`` (P, 4).  Returns ({param: grad}, d_feat (P, 64), d_zlat (P, 512) or None).
+def mlp_backward(mlp, save, d_o, P, ns=1):
+    """ResnetFC backward (resnetfc.py:132-184) given dL/d(pre-head output) ``d_o`` (P, 4),
+    for ``ns`` source views per point.  Returns ({param: grad}, d_feat (ns P, 64),
+    d_zlat (ns P, 512) or None), rows view-major like the activation save.
     The 512-wide GEMMs are fp32 hipBLASLt GEMMs (split-fp16 GEMMs assembled from torch
     ops measured 2x slower end to end: the split / scale passes cost more than they save)."""
     mm = torch.mm
     nb = mlp.n_blocks
+    nc = min(mlp.combine_layer, nb) if ns > 1 else nb
     lin_z = list(getattr(mlp, "lin_z", []))
-    feat, z, slot = _save_views(save, P, nb)
+    feat, z, slot = _save_views(save, P, nb, ns=ns)
     g = {}
-    xf = slot(2 * nb)
+    xf = slot(2 * nb, P)
     W = mlp.lin_out.weight.detach()
     g[mlp.lin_out.weight] = d_o.t() @ xf
     g[mlp.lin_out.bias] = d_o.sum(0)
@@ -67,7 +77,8 @@ def mlp_backward(mlp, save, d_o, P):
     dz = None
     for b in reversed(range(nb)):
         blk = mlp.blocks[b]
-        hb, xb = slot(nb + b), slot(b)
+        rows = ns * P if b < nc else P
+        hb, xb = slot(nb + b, rows), slot(b, rows)
         w1, w0 = blk.fc_1.weight.detach(), blk.fc_0.weight.detach()
         g[blk.fc_1.weight] = mm(dx.t(), hb)
         g[blk.fc_1.bias] = dx.sum(0)
@@ -81,10 +92,14 @@ def mlp_backward(mlp, save, d_o, P):
             g[lz.bias] = dx.sum(0)
             t = mm(dx, lz.weight.detach())
             dz = t if dz is None else dz + t
+        if b == nc and ns > 1:
+            # x = mean over views at the start of block nc (combine_interleaved): every view's
+            # row gets dL/d(mean) / ns, rows view-major
+            dx = (dx / ns).repeat(ns, 1)
     d_in = mlp.lin_in.weight.shape[1]
     g[mlp.lin_in.weight] = _tall_mm(dx, feat)[:, :d_in]
     g[mlp.lin_in.bias] = dx.sum(0)
-    d_feat = torch.zeros(P, 64, device=dx.device, dtype=torch.float32)
+    d_feat = torch.zeros(ns * P, 64, device=dx.device, dtype=torch.float32)
     d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
     return g, d_feat, dz
 
@@ -199,7 +214,8 @@ class RenderPoints(torch.autograd.Function):
         P = B * K
         lib = _lib.load()
         dev = z.device
-        n_save = lib.pnr_point_save_floats(desc, P)
+        ns = net.num_views_per_obj
+        n_save = lib.pnr_point_save_floats(desc, P * ns)
         if n_save == 0:
             _lib.check(-1, "pnr_point_save_floats")
         save = torch.empty(n_save, dtype=torch.float32, device=dev)
@@ -224,16 +240,17 @@ class RenderPoints(torch.autograd.Function):
         # head: [sigmoid(rgb), relu(sigma)] (models.py:258-265)
         d_o = torch.cat([d_out[:, :3] * out[:, :3] * (1.0 - out[:, :3]),
                          d_out[:, 3:] * (out[:, 3:] > 0)], dim=1)
-        if net.mlp_precision == "f16x3":
+        ns = net.num_views_per_obj
+        if net.mlp_precision == "f16x3" and ns == 1:
             g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P)
         else:
-            g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P)
+            g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns)
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         d_z = torch.empty(P, dtype=torch.float32, device=z.device) if need_z else None
         d_lat = torch.zeros_like(latent_cl) if need_lat else None
         if need_z or need_lat:
             if d_zlat is None:
-                d_zlat = torch.zeros(P, 512, dtype=torch.float32, device=z.device)
+                d_zlat = torch.zeros(ns * P, 512, dtype=torch.float32, device=z.device)
             lib = _lib.load()
             r = _lib.Rays(_lib.ptr(rays), B, B // net.num_objs)
             _lib.check(lib.pnr_points_input_backward(net.hip_scene(), ctx.desc, _lib.ptr(ctx.packed), r,
