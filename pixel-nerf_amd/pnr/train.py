@@ -57,13 +57,23 @@ def _save_views(save, P, n_blocks, H=512, ns=1):
     return feat, z, slot
 
 
-def mlp_backward(mlp, save, d_o, P, ns=1):
+def mlp_backward(mlp, save, d_o, P, ns=1, use_wgrad=False):
     """ResnetFC backward (resnetfc.py:132-184) given dL/d(pre-head output) ``d_o`` (P, 4),
     for ``ns`` source views per point.  Returns ({param: grad}, d_feat (ns P, 64),
     d_zlat (ns P, 512) or None), rows view-major like the activation save.
     The 512-wide GEMMs are fp32 hipBLASLt GEMMs (split-fp16 GEMMs assembled from torch
-    ops measured 2x slower end to end: the split / scale passes cost more than they save)."""
+    ops measured 2x slower end to end: the split / scale passes cost more than they save);
+    with ``use_wgrad`` the 512 x 512 weight gradients are ``pnr_weight_grad`` launches
+    instead (one per row count: ns P rows before combine_layer, P after)."""
     mm = torch.mm
+    jobs = {}   # rows -> [(param, dY, X)] for pnr_weight_grad
+
+    def wgrad(param, dy, x):
+        if use_wgrad:
+            jobs.setdefault(dy.shape[0], []).append((param, dy, x))
+        else:
+            g[param] = mm(dy.t(), x)
+
     nb = mlp.n_blocks
     nc = min(mlp.combine_layer, nb) if ns > 1 else nb
     lin_z = list(getattr(mlp, "lin_z", []))
@@ -80,15 +90,15 @@ def mlp_backward(mlp, save, d_o, P, ns=1):
         rows = ns * P if b < nc else P
         hb, xb = slot(nb + b, rows), slot(b, rows)
         w1, w0 = blk.fc_1.weight.detach(), blk.fc_0.weight.detach()
-        g[blk.fc_1.weight] = mm(dx.t(), hb)
+        wgrad(blk.fc_1.weight, dx, hb)
         g[blk.fc_1.bias] = dx.sum(0)
         dh = mm(dx, w1) * (hb > 0)
-        g[blk.fc_0.weight] = mm(dh.t(), xb)
+        wgrad(blk.fc_0.weight, dh, xb)
         g[blk.fc_0.bias] = dh.sum(0)
         dx = dx + mm(dh, w0) * (xb > 0)
         if b < len(lin_z):
             lz = lin_z[b]
-            g[lz.weight] = mm(dx.t(), z)
+            wgrad(lz.weight, dx, z)
             g[lz.bias] = dx.sum(0)
             t = mm(dx, lz.weight.detach())
             dz = t if dz is None else dz + t
@@ -101,6 +111,12 @@ def mlp_backward(mlp, save, d_o, P, ns=1):
     g[mlp.lin_in.bias] = dx.sum(0)
     d_feat = torch.zeros(ns * P, 64, device=dx.device, dtype=torch.float32)
     d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
+    for rows, js in jobs.items():
+        for i in range(0, len(js), 16):   # pnr_weight_grad: up to 16 layers per launch
+            part = js[i:i + 16]
+            gw = weight_grad([dy.contiguous() for _, dy, _ in part], [x for _, _, x in part], rows)
+            for j, (param, _, _) in enumerate(part):
+                g[param] = gw[j]
     return g, d_feat, dz
 
 
@@ -244,7 +260,7 @@ class RenderPoints(torch.autograd.Function):
         if net.mlp_precision == "f16x3" and ns == 1:
             g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P)
         else:
-            g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns)
+            g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns, use_wgrad=net.mlp_precision == "f16x3")
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         d_z = torch.empty(P, dtype=torch.float32, device=z.device) if need_z else None
         d_lat = torch.zeros_like(latent_cl) if need_lat else None

@@ -2,7 +2,8 @@
 """Training-step benchmark (BASELINE.json configs[4]).
 
 One step = the reference's train.py:182-283 on synthetic SRN-cars-shaped data:
-  * encode: the ResNet34 trunk (encoder.py:111-164) on SB source images (128x128, NS = 1);
+  * encode: the ResNet34 trunk (encoder.py:111-164) on SB x NS source images (128x128;
+    NS = --views, 1 by default as in the SRN setting, train.py -V);
   * render: SB x B' rays with the shipped conf (64 coarse + 32 fine incl. 16 depth
     samples, white background) through the HIP training path (pnr/train.py);
   * loss: MSE(coarse rgb) + MSE(fine rgb) (lambda = 1, conf/default.conf:77-78);
@@ -49,6 +50,7 @@ def main():
     ap.add_argument("--sb", type=int, default=4)
     ap.add_argument("--rays-per-obj", type=int, default=256)
     ap.add_argument("--precision", default="f16x3")
+    ap.add_argument("--views", type=int, default=1, help="source views per object (train.py -V)")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step captured as one HIP graph instead of launching every kernel "
                          "from Python (measured within 1 %% of eager: the step is GPU-bound)")
@@ -74,13 +76,16 @@ def main():
     opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=args.graph)
     params = list(net.parameters())
 
-    sb, per = args.sb, args.rays_per_obj
+    sb, per, ns = args.sb, args.rays_per_obj, args.views
     W = H = 128
     focal = torch.tensor(131.25, device=dev)
-    src_poses = synth.srn_poses([float(15 * i + 7 * rank) for i in range(sb)]).to(dev)
+    src_poses = synth.srn_poses([float(15 * i + 7 * rank + 40 * v) for i in range(sb) for v in range(ns)]).to(dev)
+    if ns > 1:
+        src_poses = src_poses.reshape(sb, ns, 4, 4)
     tgt_poses = synth.srn_poses([float(15 * i + 7 * rank + 90) for i in range(sb)]).to(dev)
     g = torch.Generator(device=dev).manual_seed(rank)
-    images = torch.rand(sb, 3, H, W, device=dev, generator=g) * 2 - 1
+    images = torch.rand(sb, 3, H, W, device=dev, generator=g) * 2 - 1 if ns == 1 else \
+        torch.rand(sb, ns, 3, H, W, device=dev, generator=g) * 2 - 1
     all_rays = util.gen_rays(tgt_poses, W, H, focal, 0.8, 1.8).reshape(sb, -1, 8)   # on device
     pix = torch.randint(0, W * H, (sb, per), device=dev, generator=g)
     rays = torch.gather(all_rays, 1, pix[..., None].expand(-1, -1, 8)).contiguous()
@@ -141,11 +146,13 @@ def main():
         "value": round(rays_total / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "dtype": "f32", "arithmetic": (args.precision + " forward + f16x3 fused input-gradient chain + split-bf16 (x6) weight gradients"
+                                                     if args.precision == "f16x3" and ns == 1 else
+                                                     args.precision + " forward + fp32 GEMM input-gradient chain + split-bf16 (x6) weight gradients"
                                                      if args.precision == "f16x3" else
                                                      args.precision + " forward, fp32 GEMM backward") + " (pnr/train.py)",
         "data": "synthetic (random source images, hash-initialised MLPs, SRN geometry)",
-        "config": {"workload": "cfg5: SB=%d objects x %d rays per rank, 64 coarse + 32 fine (16 depth)"
-                               % (sb, per), "global_batch_rays": sb * per * world,
+        "config": {"workload": "cfg5: SB=%d objects x %d rays per rank, %d source view(s), 64 coarse + 32 fine "
+                               "(16 depth)" % (sb, per, ns), "global_batch_rays": sb * per * world,
                    "parallelism": "data parallel, 1 process per GPU, bucketed RCCL all-reduce",
                    "launch": "one HIP graph per step" if args.graph else "eager"},
         "loss": round(loss.item(), 6),
