@@ -1040,6 +1040,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // ranges: a slower CU or XCD no longer leaves the rest of the chip idle at the end of
     // the launch.  The next tile is fetched before the head, so the atomic's latency hides.
     int *s_next = reinterpret_cast<int *>(petab + 32);
+    float *hpart = petab + 64;   // PREC 3 head: k-half partials [wave][lane][4] (8 KB)
     auto grab = [&]() -> int {
         const int64_t T = a.n_tiles;
         const int x0 = blockIdx.x & 7;
@@ -1330,13 +1331,17 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #ifdef PNR_GEMM_ONLY
         if (0)
 #endif
-        if (PREC == 3 && wave < CT) {
-            // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col
-            const float *wo = a.packed + L.off_lin_out + lane * 4;
-            const _Float16 *q0 = gc.pb0 + wave * 16 * ROWH, *q1 = gc.pb1 + wave * 16 * ROWH;
+        if (PREC == 3) {
+            // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col, the k range
+            // split over the 8 waves: wave w sums column tile w % 4 over k-half w / 4 into LDS;
+            // after the tile's closing barrier waves 0-3 add the two halves and apply the head
+            const int ct = wave % CT, kh = wave / CT;
+            const float *wo = a.packed + L.off_lin_out + opaque_lane(lane) * 4 + kh * (KS32 / 2) * 512;
+            const _Float16 *q0 = gc.pb0 + ct * 16 * ROWH + kh * 32 * (KS32 / 2);
+            const _Float16 *q1 = gc.pb1 + ct * 16 * ROWH + kh * 32 * (KS32 / 2);
             f4 o = {0.f, 0.f, 0.f, 0.f}, o2 = o;
-#pragma unroll 4
-            for (int ks = 0; ks < KS32; ks += 2) {
+#pragma unroll
+            for (int ks = 0; ks < KS32 / 2; ks += 2) {
                 const h8 w0 = *reinterpret_cast<const h8 *>(wo + ks * 512);
                 const h8 w1 = *reinterpret_cast<const h8 *>(wo + ks * 512 + 256);
                 const h8 v0 = *reinterpret_cast<const h8 *>(q0 + 32 * ks);
@@ -1352,18 +1357,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 o = mfma_h(w0, v0, o);
                 o2 = mfma_h(w2, v2, o2);
             }
-            const int e = ecol[16 * wave + cl] + (int)a.packed[HDR_ESCALE + 1 + L.n_l512];
-            const f4 b = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * g);
-            o = (o + o2) * __builtin_ldexpf(1.f, -e) + b;
-            const int64_t po = tile * COLS + 16 * wave + cl;
-            if (g == 0 && po < a.n_points) {
-                f4 r;
-                r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
-                r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
-                r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
-                r.w = fmaxf(o.w, 0.f);
-                *reinterpret_cast<f4 *>(a.out + po * 4) = r;
-            }
+            *reinterpret_cast<f4 *>(hpart + (wave * 64 + opaque_lane(lane)) * 4) = o + o2;
         } else if (PREC != 3 && wave < CT) {   // wave-uniform: the first CT waves own one column tile each
             const float *wo = a.packed + L.off_lin_out + lane * 4;
             const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
@@ -1391,7 +1385,24 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
         PT(gc, 4);
         PT_COUNT(gc, 6);
-        __syncthreads();   // s_next written; every wave leaves the head before the next tile
+        __syncthreads();   // s_next and the head partials written
+        if (PREC == 3 && wave < CT) {   // [sigmoid(rgb), relu(sigma)] of column tile `wave`
+            const int ln = opaque_lane(lane), gg = ln >> 4, cc = ln & 15;
+            const f4 h0 = *reinterpret_cast<const f4 *>(hpart + (wave * 64 + ln) * 4);
+            const f4 h1 = *reinterpret_cast<const f4 *>(hpart + ((wave + CT) * 64 + ln) * 4);
+            const int e = ecol[16 * wave + cc] + (int)a.packed[HDR_ESCALE + 1 + L.n_l512];
+            const f4 b = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * gg);
+            const f4 o = (h0 + h1) * __builtin_ldexpf(1.f, -e) + b;
+            const int64_t po = tile * COLS + 16 * wave + cc;
+            if (gg == 0 && po < a.n_points) {
+                f4 r;
+                r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
+                r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
+                r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
+                r.w = fmaxf(o.w, 0.f);
+                *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+            }
+        }
     }
 #ifdef PNR_PHASE_TIMING
     if (threadIdx.x == 0)
@@ -1766,7 +1777,7 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     //         = 143,760 B; else: fp32 activations + staging ring + gather records + PE table +
     //         next tile = 158,864 B
     const size_t lds = d.precision == PNR_PREC_F16X3
-        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS + 32 + 4)
+        ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS + 64 + 2048)
         : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8 + 32 + 4);
 #define PNR_LAUNCH_MLP(P)                                                                              \
     do {                                                                                               \
