@@ -210,7 +210,7 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P):
         g[lz.bias] = sums[nb + b]
     dx = dy[nb]
     d_in = mlp.lin_in.weight.shape[1]
-    g[mlp.lin_in.weight] = dx.t() @ feat[:, :d_in]
+    g[mlp.lin_in.weight] = _tall_mm(dx, feat)[:, :d_in]
     g[mlp.lin_in.bias] = sums[nb]
     d_feat = torch.zeros(P, 64, device=dev, dtype=torch.float32)
     d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
