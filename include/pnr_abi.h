@@ -313,6 +313,19 @@ int pnr_mlp_backward(const pnr_mlp_desc *desc, const void *packed, const void *p
                      const float *lin_out_w, const float *save, const float *d_o, int64_t n_points,
                      float *dy, float *d_zlat, pnr_stream_t stream);
 
+/* Workspace bytes of pnr_mlp_backward_bias for n_points points (0 if n_points <= 0). */
+size_t pnr_mlp_backward_workspace_bytes(const pnr_mlp_desc *desc, int64_t n_points);
+
+/* pnr_mlp_backward plus the ResnetFC bias gradients (resnetfc.py:132-184: the column sums of
+ * the dy slots over the points) in the same pass: d_bias ((2 n_blocks + 1), 512) in dy's slot
+ * order, summed per workgroup over its tiles and then over the workgroups, both in a fixed
+ * order (deterministic).  d_bias NULL = pnr_mlp_backward; otherwise `workspace` holds
+ * pnr_mlp_backward_workspace_bytes. */
+int pnr_mlp_backward_bias(const pnr_mlp_desc *desc, const void *packed, const void *packed_t,
+                          const float *lin_out_w, const float *save, const float *d_o, int64_t n_points,
+                          float *dy, float *d_zlat, float *d_bias, void *workspace, size_t workspace_bytes,
+                          pnr_stream_t stream);
+
 /* Workspace bytes of pnr_weight_grad (n_layers in 1..16); 0 if the sizes are invalid. */
 size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points);
 

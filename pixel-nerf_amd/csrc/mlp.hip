@@ -1433,13 +1433,25 @@ struct BwdArgs {
     const float *d_o;        // (P, 4) gradient of the pre-head output
     float *dy;               // (2 nb + 1) x P x 512
     float *dzlat;            // (P, 512) gradient of the sampled latent (n_linz > 0)
+    float *bsum;             // NULL, or [workgroup][2 nb + 1][512] column sums of each dy slot
+                             // over the workgroup's tiles (its tiles in order: deterministic)
     Layout L;
     int64_t n_points, n_tiles;
 };
 
+// sum over the 16 lanes of a DPP row (every lane gets it; lane 0's order is the fixed tree
+// ((a + a8) + (a4 + a12)) + ...)
+__device__ __forceinline__ float row16_sum(float v) {
+    v += dpp_f<0x128>(0.f, v);   // row_ror:8
+    v += dpp_f<0x124>(0.f, v);   // row_ror:4
+    v += dpp_f<0x122>(0.f, v);   // row_ror:2
+    v += dpp_f<0x121>(0.f, v);   // row_ror:1
+    return v;
+}
+
 // this wave's rows of acc -> slot [point][512] (points < n_points)
 __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
-                                           int wave, int lane) {
+                                           int wave, int lane, float *bs = nullptr, bool first = false) {
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
@@ -1449,6 +1461,26 @@ __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t 
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = acc[r][c];
+    }
+    if (bs) {   // bias gradient: this tile's column sums of the wave's rows, added to bs
+        f4 sr[RTW];
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+            f4 t = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+                if (tile * COLS + 16 * c + cl < n_points) t += acc[r][c];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) t[e] = row16_sum(t[e]);
+            sr[r] = t;
+        }
+        if (cl == 0) {
+#pragma unroll
+            for (int r = 0; r < RTW; ++r) {
+                f4 *q = reinterpret_cast<f4 *>(bs + 16 * (RTW * wave + r) + 4 * g);
+                *q = first ? sr[r] : *q + sr[r];
+            }
+        }
     }
 }
 // relu backward masks from the forward's sign bits (save_mask): this lane's two words of
@@ -1511,6 +1543,9 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     auto mask_slot = [&](int i) { return msk + P * 16 * i; };
     u2m mk[CT];
     auto dy_slot = [&](int i) { return a.dy + P * H * i; };
+    auto bs_slot = [&](int i) -> float * {
+        return a.bsum ? a.bsum + ((int64_t)blockIdx.x * (2 * nb + 1) + i) * H : nullptr;
+    };
     auto publish = [&](const Acc &acc) {
         // no barrier first: the column maxima are written before the internal barrier and the
         // image after it, when every wave has left the GEMM that read the previous image
@@ -1550,13 +1585,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
         bool published = false;
         for (int b = nb - 1; b >= 0; --b) {
             if (!published) publish(x);
-            store_rows(x, dy_slot(nb + 1 + b), tile, P, wave, lane);
+            store_rows(x, dy_slot(nb + 1 + b), tile, P, wave, lane, bs_slot(nb + 1 + b), tile == blockIdx.x);
             const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
             zero(h);
             load_mask(mk, mask_slot(nb + b), tile, P, wave, lane);   // lands during the GEMM
             layer_gemm<3, NKB, H_DIST_3>(h, layer(l1), gc, 1 + l1);
             relu_mask(h, mk, tile, P, lane);
-            store_rows(h, dy_slot(b), tile, P, wave, lane);
+            store_rows(h, dy_slot(b), tile, P, wave, lane, bs_slot(b), tile == blockIdx.x);
             publish(h);
             zero(h);
             load_mask(mk, mask_slot(b), tile, P, wave, lane);
@@ -1587,8 +1622,17 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                 }
             }
         }
-        store_rows(x, dy_slot(nb), tile, P, wave, lane);
+        store_rows(x, dy_slot(nb), tile, P, wave, lane, bs_slot(nb), tile == blockIdx.x);
     }
+}
+
+// d_bias[i] = sum over the workgroups (in order) of their column-sum partials
+__global__ void k_bias_reduce(const float *__restrict__ part, int n_wg, int n, float *__restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    float s = part[t];
+    for (int w = 1; w < n_wg; ++w) s += part[(int64_t)w * n + t];
+    out[t] = s;
 }
 
 }  // namespace mlpk
@@ -1707,8 +1751,20 @@ int mlp_pack_t(const pnr_mlp_weights &w, const void *packed, void *packed_t, siz
     return launch_ok("mlp_pack_t") ? PNR_OK : PNR_ERR_HIP;
 }
 
+static int64_t mlp_bwd_grid(int64_t n_points) {
+    const int64_t tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
+    const int cus = device_cu_count();
+    return tiles < cus ? tiles : cus;
+}
+
+size_t mlp_bwd_workspace_bytes(const pnr_mlp_desc &d, int64_t n_points) {
+    if (n_points <= 0) return 0;
+    return sizeof(float) * (size_t)mlp_bwd_grid(n_points) * (2 * d.n_blocks + 1) * mlpk::H;
+}
+
 int launch_mlp_bwd(const pnr_mlp_desc &d, const void *packed, const void *packed_t, const float *w_out,
-                   const float *save, const float *d_o, int64_t n_points, float *dy, float *dzlat, hipStream_t st) {
+                   const float *save, const float *d_o, int64_t n_points, float *dy, float *dzlat, hipStream_t st,
+                   float *d_bias, void *ws, size_t ws_bytes) {
     int rc = mlp_check_desc(d);
     if (rc) return rc;
     if (d.precision != PNR_PREC_F16X3)
@@ -1726,12 +1782,23 @@ int launch_mlp_bwd(const pnr_mlp_desc &d, const void *packed, const void *packed
     a.dzlat = dzlat;
     a.n_points = n_points;
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
-    const int cus = device_cu_count();
-    const int64_t grid = a.n_tiles < cus ? a.n_tiles : cus;
+    const int64_t grid = mlp_bwd_grid(n_points);
+    if (d_bias) {
+        const size_t need = mlp_bwd_workspace_bytes(d, n_points);
+        if (!ws || ws_bytes < need) return fail(PNR_ERR_WORKSPACE, "mlp backward: workspace %zu < %zu", ws_bytes, need);
+        a.bsum = static_cast<float *>(ws);
+    }
     // split image P0 + P1, column maxima, exponents = 137,472 B
     const size_t lds = 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (mlpk::COLS * 8 + mlpk::COLS);
     hipLaunchKernelGGL(mlpk::k_mlp_bwd, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
-    return launch_ok("mlp_bwd") ? PNR_OK : PNR_ERR_HIP;
+    if (!launch_ok("mlp_bwd")) return PNR_ERR_HIP;
+    if (d_bias) {
+        const int n = (2 * d.n_blocks + 1) * mlpk::H;
+        hipLaunchKernelGGL(mlpk::k_bias_reduce, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a.bsum,
+                           (int)grid, n, d_bias);
+        if (!launch_ok("bias_reduce")) return PNR_ERR_HIP;
+    }
+    return PNR_OK;
 }
 
 int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points) {

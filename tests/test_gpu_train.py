@@ -179,16 +179,19 @@ def test_training_noise_std_draw_order_matches_reference():
     assert torch.isfinite(lat.grad).all()
 
 
-def test_fused_mlp_backward_matches_torch_backward():
-    """pnr_mlp_backward (the f16x3 W^T chain: masks, residuals, lin_z latent gradient) plus
-    the batched weight GEMMs against the per-layer fp32 torch backward (train.mlp_backward)
-    on the same activation save: 7,872 points (ragged last tile), per-point gradient
-    magnitudes spread over 2^-20 .. 1.  Tolerance 2e-5 of each tensor's max-abs."""
+@pytest.mark.parametrize("rays_per_obj,K", [(96, 41), (256, 64)])
+def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K):
+    """pnr_mlp_backward_bias (the f16x3 W^T chain: masks, residuals, lin_z latent gradient,
+    bias column sums) plus the batched weight GEMMs against the per-layer fp32 torch backward
+    (train.mlp_backward) on the same activation save: 7,872 points (ragged last tile, one
+    tile per workgroup) and 32,768 (several tiles per workgroup: the bias partials add up
+    across tiles), per-point gradient magnitudes spread over 2^-20 .. 1.  Tolerance 2e-5 of
+    each tensor's max-abs."""
     from types import SimpleNamespace
 
     from pnr import train
 
-    cs = case(sb=2, rays_per_obj=96, kc=41)
+    cs = case(sb=2, rays_per_obj=rays_per_obj, kc=K)
     net = PixelNeRFNet(conf())
     net.load_state_dict(cs["sd"], strict=False)
     net = net.to(DEV)
@@ -196,7 +199,6 @@ def test_fused_mlp_backward_matches_torch_backward():
     net.encode_latent(cs["latent"].to(DEV), cs["poses"].to(DEV), cs["focal"].to(DEV),
                       (cs["width"], cs["height"]), c=cs["c"].to(DEV), num_objs=cs["poses"].shape[0])
     rays = cs["rays"].to(DEV).reshape(-1, 8).contiguous()
-    K = 41
     t = torch.linspace(0.0, 1.0, K, device=DEV)
     z = (rays[:, 6:7] + (rays[:, 7:8] - rays[:, 6:7]) * t).contiguous()
     ctx = SimpleNamespace()
