@@ -22,6 +22,51 @@ from .consts import device_const
 __all__ = ["SpatialEncoder", "resnet34_trunk"]
 
 
+def _latent_channels_last(maps):
+    from . import _lib
+
+    maps = [t.contiguous().float() for t in maps]
+    n, (h, w) = maps[0].shape[0], maps[0].shape[-2:]
+    c_total = sum(t.shape[1] for t in maps)
+    out = torch.empty(n, h, w, c_total, dtype=torch.float32, device=maps[0].device)
+    k = len(maps)
+    ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in maps])
+    ch = (ctypes.c_int32 * k)(*[t.shape[1] for t in maps])
+    hs = (ctypes.c_int32 * k)(*[t.shape[2] for t in maps])
+    ws = (ctypes.c_int32 * k)(*[t.shape[3] for t in maps])
+    _lib.check(_lib.load().pnr_latent_channels_last(ptrs, ch, hs, ws, k, n, _lib.ptr(out), h, w,
+                                                     _lib.stream_of(out.device)),
+               "pnr_latent_channels_last")
+    return out
+
+
+class LatentChannelsLast(torch.autograd.Function):
+    """(n, h, w, sum C_i) = cat_i(upsample_bilinear_align_corners(map_i, (h, w))) channels-last
+    (encoder.py:150-160) in one HIP kernel; the backward is each map's bilinear-upsample
+    adjoint on its channel slice of the incoming gradient (what autograd of F.interpolate +
+    torch.cat runs)."""
+
+    @staticmethod
+    def forward(ctx, *maps):
+        ctx.shapes = [tuple(t.shape) for t in maps]
+        return _latent_channels_last(maps)
+
+    @staticmethod
+    def backward(ctx, g):
+        gn = g.permute(0, 3, 1, 2)   # NCHW view of the channels-last gradient
+        h, w = gn.shape[-2:]
+        grads, c0 = [], 0
+        for shp in ctx.shapes:
+            gi = gn[:, c0:c0 + shp[1]]
+            c0 += shp[1]
+            if tuple(shp[-2:]) == (h, w):
+                grads.append(gi.contiguous())
+            else:
+                grads.append(torch.ops.aten.upsample_bilinear2d_backward(
+                    gi, [h, w], list(shp), True, None, None))
+        return tuple(grads)
+
+
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -147,8 +192,7 @@ class SpatialEncoder(nn.Module):
         if self.num_layers > 4:
             x = m.layer4(x)
             latents.append(x)
-        if (x.is_cuda and not (torch.is_grad_enabled() and x.requires_grad)
-                and self.upsample_interp == "bilinear" and len(latents) <= 8):
+        if x.is_cuda and self.upsample_interp == "bilinear" and len(latents) <= 8:
             return self.set_latent_maps(latents)
         size = latents[0].shape[-2:]
         for i in range(len(latents)):
@@ -160,21 +204,10 @@ class SpatialEncoder(nn.Module):
         """encoder.py:150-163 on the HIP device without the NCHW concat + transpose:
         ``pnr_latent_channels_last`` upsamples (bilinear, align_corners) and concatenates
         the trunk maps straight into the channels-last latent the ray march reads;
-        ``latent`` is its NCHW view (no copy)."""
-        from . import _lib
-
-        maps = [t.contiguous().float() for t in maps]
-        n, (h, w) = maps[0].shape[0], maps[0].shape[-2:]
-        c_total = sum(t.shape[1] for t in maps)
-        out = torch.empty(n, h, w, c_total, dtype=torch.float32, device=maps[0].device)
-        k = len(maps)
-        ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in maps])
-        ch = (ctypes.c_int32 * k)(*[t.shape[1] for t in maps])
-        hs = (ctypes.c_int32 * k)(*[t.shape[2] for t in maps])
-        ws = (ctypes.c_int32 * k)(*[t.shape[3] for t in maps])
-        _lib.check(_lib.load().pnr_latent_channels_last(ptrs, ch, hs, ws, k, n, _lib.ptr(out), h, w,
-                                                         _lib.stream_of(out.device)),
-                   "pnr_latent_channels_last")
+        ``latent`` is its NCHW view (no copy).  Under autograd the gradient flows back
+        through each map's upsample adjoint (``LatentChannelsLast``)."""
+        out = LatentChannelsLast.apply(*maps)
+        h, w = out.shape[1], out.shape[2]
         self.latent = out.permute(0, 3, 1, 2)
         ls = device_const((w, h), out.device)
         self.latent_scaling = ls / (ls - 1) * 2.0

@@ -1,9 +1,11 @@
 #!/bin/bash
 # Training bench A/B in one box session: the working tree vs a copy of it whose pnr/train.py
-# is replaced by pixel-nerf_amd/build/old_train.py (written locally from a git revision).
+# (or AB_FILE=pnr/<name>.py) is replaced by pixel-nerf_amd/build/old_<name>.py (written
+# locally from a git revision).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OLD=/tmp/pnr_old_repo
-rm -rf $OLD && cp -r . $OLD && cp pixel-nerf_amd/build/old_train.py $OLD/pixel-nerf_amd/pnr/train.py || exit 1
+F=${AB_FILE:-pnr/train.py}
+rm -rf $OLD && cp -r . $OLD && cp pixel-nerf_amd/build/old_$(basename $F) $OLD/pixel-nerf_amd/$F || exit 1
 for round in 1 2; do
   for v in old new; do
     root=.; [ $v = old ] && root=$OLD

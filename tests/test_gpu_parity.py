@@ -457,6 +457,29 @@ def test_frame_render_matches_reference_gen_video():
 
 
 # --------------------------------------------------------------- encoder --
+def test_latent_channels_last_backward_matches_torch_autograd():
+    """LatentChannelsLast (the training encoder's upsample + concat, encoder.py:150-160, as one
+    HIP kernel) against autograd of F.interpolate(align_corners) + torch.cat + the
+    channels-last permute: forward and the gradient of every trunk map."""
+    import torch.nn.functional as F
+
+    from pnr.encoder import LatentChannelsLast
+
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    shapes = [(2, 64, 32, 40), (2, 64, 16, 20), (2, 128, 8, 10), (2, 256, 4, 5)]
+    maps = [torch.randn(sh, generator=gen).to(DEV).requires_grad_(True) for sh in shapes]
+    out = LatentChannelsLast.apply(*maps)
+    ref = torch.cat([F.interpolate(m, (32, 40), mode="bilinear", align_corners=True) for m in maps],
+                    1).permute(0, 2, 3, 1)
+    assert (out - ref).abs().max().item() <= 1e-6 * max(1.0, ref.abs().max().item())
+    g = torch.randn(out.shape, generator=gen).to(DEV)
+    got = torch.autograd.grad(out, maps, g)
+    want = torch.autograd.grad(ref, maps, g)
+    for a, b in zip(got, want):
+        assert a.shape == b.shape
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item(), (a - b).abs().max().item()
+
+
 def test_latent_channels_last_matches_torch_upsample_concat():
     """pnr_latent_channels_last (encoder.py:150-160 tail) vs the
     reference's F.interpolate(bilinear, align_corners=True) + cat, transposed; and a no-grad
