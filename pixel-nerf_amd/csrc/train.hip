@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
 //       weights (out-of-range corners count as 0; clipped coordinates pass no gradient,
 //       as torch's grid_sampler_2d_backward with border padding)
 // Consecutive samples of a ray often fall in the same latent cell, so the wave keeps the
-// four corner gradients of the current cell in registers (lane = 8 channels per corner)
+// four corner gradients of the current cell in registers (lane = 8 channels per corner,
+// lane-contiguous so each atomic instruction touches 2 cache lines)
 // and flushes them with atomics only when the cell changes: one atomic per channel and
 // corner per run of equal cells instead of per point.  The dL/dz chains of the run's
 // points are computed afterwards by lanes 0 .. RUN-1 in parallel.
@@ -200,13 +201,14 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
             if (cur < 0 || !d_latent) return;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                const int ch = half * 256 + lane * 4;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    atomicAdd(d_latent + cur + ch + q, acc[0][half][q]);
-                    if (cur_x1) atomicAdd(d_latent + c01 + ch + q, acc[1][half][q]);
-                    if (cur_y1) atomicAdd(d_latent + c10 + ch + q, acc[2][half][q]);
-                    if (cur_x1 && cur_y1) atomicAdd(d_latent + c11 + ch + q, acc[3][half][q]);
+                    // lane-contiguous channels: one atomic instruction covers 256 B (2 lines)
+                    const int ch = half * 256 + q * 64 + lane;
+                    atomicAdd(d_latent + cur + ch, acc[0][half][q]);
+                    if (cur_x1) atomicAdd(d_latent + c01 + ch, acc[1][half][q]);
+                    if (cur_y1) atomicAdd(d_latent + c10 + ch, acc[2][half][q]);
+                    if (cur_x1 && cur_y1) atomicAdd(d_latent + c11 + ch, acc[3][half][q]);
                 }
             }
         };
@@ -229,12 +231,18 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
             const float *gz = d_zlat + (v * n_points + p) * 512;
 #pragma unroll
             for (int half = 0; half < 2; ++half) {
-                const int ch = half * 256 + lane * 4;
-                const f4 gv = *reinterpret_cast<const f4 *>(gz + ch);
-                const f4 l00 = *reinterpret_cast<const f4 *>(latent + G.o00 + ch);
-                f4 l01 = *reinterpret_cast<const f4 *>(latent + G.o01 + ch);
-                f4 l10 = *reinterpret_cast<const f4 *>(latent + G.o10 + ch);
-                f4 l11 = *reinterpret_cast<const f4 *>(latent + G.o11 + ch);
+                // channel half * 256 + q * 64 + lane (q = vector element): coalesced 256-B rows
+                // per load, and the same lane-contiguous layout for the flush atomics
+                const int ch = half * 256 + lane;
+                f4 gv, l00, l01, l10, l11;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    gv[q] = gz[ch + q * 64];
+                    l00[q] = latent[G.o00 + ch + q * 64];
+                    l01[q] = latent[G.o01 + ch + q * 64];
+                    l10[q] = latent[G.o10 + ch + q * 64];
+                    l11[q] = latent[G.o11 + ch + q * 64];
+                }
                 if (!G.inx1) { l01 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l01; }
                 if (!G.iny1) { l10 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l10; }
 #pragma unroll
