@@ -150,13 +150,20 @@ def psnr_vs_reference_path(net, rays_dev, ref, streams, dev):
     injected random streams, against the oracle's render of them (oracle/ref_cpu.py, the
     CPU restatement pinned to the reference).  `agreement_db` = PSNR(HIP, oracle);
     `delta_db` = PSNR(HIP, target) - PSNR(oracle, target) for a seeded U(0,1) target image
-    (no ground-truth frames offline)."""
+    (no ground-truth frames offline).  Fine-pass rays are excluded from the `_excl_flips`
+    figures only for a searchsorted bin flip PROVEN from the two sets of coarse weights
+    (oracle/parity.py); `unexplained_rays` (fine samples that differ without one) must be 0."""
+    from oracle import parity
+
     n = rays_dev.shape[0]
     r = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True).to(dev)
     r.streams = tuple(t.to(dev) for t in streams)
+    r.return_z = True
     with torch.no_grad():
-        out = r(net, rays_dev[None].contiguous())
+        out = r(net, rays_dev[None].contiguous(), want_weights=True)
     tgt = torch.from_numpy(synth.hash_uniform(5, n * 3).astype("float32")).reshape(n, 3)
+    cls = parity.classify_fine(out.coarse.weights[0], ref["coarse"]["weights"][0], streams[1],
+                               out.fine.z[0], ref["fine"]["z"])
 
     def psnr(a, b):   # util.psnr (util.py:474-481), +inf for identical images
         return float("inf") if float(((a - b) ** 2).mean()) == 0.0 else float(util.psnr(a, b))
@@ -166,19 +173,22 @@ def psnr_vs_reference_path(net, rays_dev, ref, streams, dev):
         mine = getattr(out, name).rgb[0].float().cpu()
         theirs = ref[name]["rgb"][0].float()
         agree = psnr(mine, theirs)
-        # rays whose fine-bin choice (inverse-CDF sample, a4) differs under
-        # fp32-level weight differences are reported and excluded from the second figure
-        flip = (mine - theirs).abs().amax(-1) > 1e-4
+        flip = cls["flip"] if name == "fine" else torch.zeros(n, dtype=torch.bool)
         keep = ~flip
         agree_kept = psnr(mine[keep], theirs[keep]) if bool(keep.any()) else float("inf")
+        d = (mine - theirs).abs()
         res[name] = dict(agreement_db=round(agree, 2) if agree < float("inf") else None,
                          delta_db=round(psnr(mine, tgt) - psnr(theirs, tgt), 6),
-                         max_abs_rgb=float((mine - theirs).abs().max()),
+                         max_abs_rgb=float(d.max()),
                          bin_flip_rays=int(flip.sum()),
                          agreement_db_excl_flips=round(agree_kept, 2) if agree_kept < float("inf") else None,
-                         max_abs_rgb_excl_flips=float((mine[keep] - theirs[keep]).abs().max())
-                         if bool(keep.any()) else 0.0)
+                         max_abs_rgb_excl_flips=float(d[keep].max()) if bool(keep.any()) else 0.0,
+                         rays_outside_tol_excl_flips=int(((d > 5e-5 + 1e-5 * theirs.abs()).any(-1) & keep).sum()))
+    res["fine"]["flip_rays"] = cls["flip_idx"][:16]
+    res["fine"]["unexplained_rays"] = int(cls["unexplained"].sum())
     res["rays"] = n
+    res["flip_rule"] = ("fine-bin flip = searchsorted bins recomputed from the HIP and the oracle "
+                        "coarse weights with the same u differ (oracle/parity.py)")
     return res
 
 

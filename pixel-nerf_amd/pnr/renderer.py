@@ -78,6 +78,9 @@ class NeRFRenderer(torch.nn.Module):
         self.register_buffer("last_sched", torch.tensor(0, dtype=torch.long), persistent=True)
         # test / benchmark hook: explicit (u_coarse, u_fine, u_fine_jit, n_depth)
         self.streams = None
+        # test / benchmark hook: add each pass's sample depths ``z`` (SB, B', K) to the
+        # output dicts (fine-pass parity is classified on them, oracle/parity.py)
+        self.return_z = False
 
     # ---- random streams (nerf.py:111, 135, 141, 158) ---------------------------------
     def draw_streams(self, n_rays, device):
@@ -188,7 +191,7 @@ class NeRFRenderer(torch.nn.Module):
         z_c = ops.sample_coarse(rays, kc, u_c, self.lindisp)
         raw_c = add_noise(RenderPoints.apply(net, True, rays, z_c, lat, *p_c))
         w_c, rgb_c, d_c = Composite.apply(z_c, raw_c.contiguous(), rays, self.white_bkgd)
-        outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, d_c, sb, want_weights))
+        outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, d_c, sb, want_weights, z_c))
         if kf > 0:
             nf = kf - kfd
             if lazy:
@@ -207,13 +210,15 @@ class NeRFRenderer(torch.nn.Module):
             p_f = mlp_params(net.mlp_fine) if net.mlp_fine is not None else p_c
             raw_f = add_noise(RenderPoints.apply(net, False, rays, z_f, lat, *p_f))
             w_f, rgb_f, d_f = Composite.apply(z_f, raw_f.contiguous(), rays, self.white_bkgd)
-            outputs.fine = self._pack_out(w_f, rgb_f, d_f, sb, want_weights)
+            outputs.fine = self._pack_out(w_f, rgb_f, d_f, sb, want_weights, z_f)
         return outputs
 
-    def _pack_out(self, w, rgb, depth, sb, want_weights):
+    def _pack_out(self, w, rgb, depth, sb, want_weights, z=None):
         d = DotMap(rgb=rgb.reshape(sb, -1, 3), depth=depth.reshape(sb, -1))
         if want_weights:
             d.weights = w.reshape(sb, -1, w.shape[-1])
+        if self.return_z and z is not None:
+            d.z = z.reshape(sb, -1, z.shape[-1])
         return d
 
     def _forward_fused(self, net, rays, sb, streams, want_weights):
@@ -240,11 +245,15 @@ class NeRFRenderer(torch.nn.Module):
         f_rgb = torch.empty(B, 3, **f32) if kf > 0 else None
         f_depth = torch.empty(B, **f32) if kf > 0 else None
         f_w = torch.empty(B, kc + kf, **f32) if (want_weights and kf > 0) else None
+        z_c = torch.empty(B, kc, **f32) if self.return_z else None
+        z_f = torch.empty(B, kc + kf, **f32) if (self.return_z and kf > 0) else None
         out = _lib.RenderOut(c_rgb.data_ptr(), c_depth.data_ptr(),
                              c_w.data_ptr() if c_w is not None else None,
                              f_rgb.data_ptr() if f_rgb is not None else None,
                              f_depth.data_ptr() if f_depth is not None else None,
-                             f_w.data_ptr() if f_w is not None else None, None, None)
+                             f_w.data_ptr() if f_w is not None else None,
+                             z_c.data_ptr() if z_c is not None else None,
+                             z_f.data_ptr() if z_f is not None else None)
         r = _lib.Rays(rays.data_ptr(), B, B // sb)
         rng = _lib.Rng(u_c.data_ptr(), u_f.data_ptr() if u_f.numel() else None,
                        u_j.data_ptr() if u_j.numel() else None,
@@ -255,21 +264,21 @@ class NeRFRenderer(torch.nn.Module):
         _lib.check(lib.pnr_render_forward_proj(sc, desc, _lib.ptr(pc), _lib.ptr(pf), _lib.ptr(zc), _lib.ptr(zf),
                                                r, rng, cfg, out, _lib.ptr(ws), ws_bytes,
                                                _lib.stream_of(dev), None), "pnr_render_forward_proj")
-        outputs = DotMap(coarse=self._pack_out(c_w, c_rgb, c_depth, sb, want_weights))
+        outputs = DotMap(coarse=self._pack_out(c_w, c_rgb, c_depth, sb, want_weights, z_c))
         if kf > 0:
-            outputs.fine = self._pack_out(f_w, f_rgb, f_depth, sb, want_weights)
+            outputs.fine = self._pack_out(f_w, f_rgb, f_depth, sb, want_weights, z_f)
         return outputs
 
     def _forward_callback(self, model, rays, sb, streams, want_weights):
         u_c, u_f, u_j, n_d = streams
         z_c = self.sample_coarse(rays, u_c)
         w_c, rgb_c, depth_c = self.composite(model, rays, z_c, coarse=True, sb=sb)
-        outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, depth_c, sb, want_weights))
+        outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, depth_c, sb, want_weights, z_c))
         if self.using_fine:
             z_f = ops.sample_fine(rays, z_c, w_c.detach(), depth_c, self.n_fine, self.n_fine_depth,
                                   self.depth_std, u_f, u_j, n_d, self.lindisp)
             w_f, rgb_f, depth_f = self.composite(model, rays, z_f, coarse=False, sb=sb)
-            outputs.fine = self._pack_out(w_f, rgb_f, depth_f, sb, want_weights)
+            outputs.fine = self._pack_out(w_f, rgb_f, depth_f, sb, want_weights, z_f)
         return outputs
 
     # ---- schedule / construction / parallel (nerf.py:318-371) ------------------------

@@ -163,6 +163,34 @@ def scene_srn(seed=0, n_rays=256, width=128, height=128, focal=131.25, theta_src
     )
 
 
+def scene_nmr(seed=0, n_rays=128, size=64, focal=70.0, theta_src=0.0, theta_tgt=45.0,
+              near=1.2, far=4.0, radius=2.7, channels=512, pick="hash"):
+    """ShapeNet-NMR-like single-view scene: 64x64 images, the latent
+    at half resolution (32x32, use_first_pool=False, conf/exp/sn64.conf:4-8), near/far
+    1.2/4.0 (DVRDataset.py:26-27), a synthetic focal of ~70 px, cameras on a sphere of
+    radius 2.7.  ``pick`` as scene_srn ("hash" = n_rays hashed pixels, "all" = prefix)."""
+    src = srn_poses([theta_src], phi=-20.0, radius=radius)
+    tgt = srn_poses([theta_tgt], phi=-20.0, radius=radius)
+    rays = util.gen_rays(tgt, size, size, torch.tensor(focal), near, far).reshape(-1, 8)
+    if pick == "hash":
+        idx = (hash_uniform(seed + 29, n_rays) * rays.shape[0]).astype(np.int64)
+        rays = rays[torch.from_numpy(idx)]
+    else:
+        rays = rays[:n_rays]
+    return dict(
+        latent=latent(seed, 1, channels, size // 2, size // 2),
+        poses=src,
+        focal=torch.tensor(focal, dtype=torch.float32),
+        c=None,
+        width=size,
+        height=size,
+        rays=rays.contiguous(),
+        near=near,
+        far=far,
+        latent_seed=seed,
+    )
+
+
 def scene_multiview(seed=0, n_views=3, n_rays=64, width=400, height=300,
                     focal=(300.0, 310.0), c=(195.0, 152.0), near=0.1, far=5.0,
                     channels=512, h_l=150, w_l=200, radius=2.0):

@@ -369,6 +369,16 @@ def frame_case(name, *, seed=1, size=32, rng_seed=8):
     rays = util.gen_rays(synth.srn_poses([40.0]), size, size, focal, 0.01, 4.0)   # (1, H, W, 8)
     B = size * size
     u_c, u_f, u_j, n_d = synth.rng_streams(rng_seed, B, 64, 32, 16)
+    # what each composite pass saw and produced (fine-pass flips are classified on them)
+    captured = []
+    orig_composite = renderer.composite
+
+    def spy_composite(model, rays_, z_samp, coarse=True, sb=0):
+        res = orig_composite(model, rays_, z_samp, coarse=coarse, sb=sb)
+        captured.append((z_samp.detach().clone(), res[0].detach().clone()))
+        return res
+
+    renderer.composite = spy_composite
     with torch.no_grad(), injected_rng(u_c, u_f, u_j, n_d):
         rgb, depth = render_par(rays.view(-1, 8)[None])
     frames = rgb[0].view(-1, size, size, 3)
@@ -377,7 +387,9 @@ def frame_case(name, *, seed=1, size=32, rng_seed=8):
     return cfg, dict(rays=rays.numpy(), poses=sc["poses"].numpy(), focal=np.asarray(sc["focal"]),
                      u_coarse=u_c.numpy(), u_fine=u_f.numpy(), u_fine_jit=u_j.numpy(),
                      n_depth=n_d.numpy(), frames=frames.numpy(), depth=depth[0].numpy(),
-                     frames_u8=(frames.numpy() * 255).astype(np.uint8))
+                     frames_u8=(frames.numpy() * 255).astype(np.uint8),
+                     coarse_weights=captured[0][1].numpy(),
+                     z_fine=captured[1][0].numpy())
 
 
 def gen_rays_case(name):
@@ -460,11 +472,23 @@ def main():
                           n_coarse=32, n_fine=0, n_fine_depth=0, white_bkgd=True,
                           rng_seed=9, with_fine=False))
     if want("fw_dtu_ns3"):
-        sc = synth.scene_multiview(seed=8, n_views=3, n_rays=16, h_l=30, w_l=40)
+        # cfg4 geometry at full size per view: latent (3, 512, 150, 200), 400x300 images
+        sc = synth.scene_multiview(seed=8, n_views=3, n_rays=64, h_l=150, w_l=200)
         save(*render_case("fw_dtu_ns3", d_hidden=512, d_latent=512, seed=2, scene=sc,
                           n_coarse=64, n_fine=64, n_fine_depth=0, white_bkgd=False,
                           rng_seed=5, multi_obj_poses=sc["poses"][None],
                           focal_override=sc["focal"][None], c_override=sc["c"][None]))
+    if want("fw_cfg3_nmr"):
+        # cfg3: ShapeNet-NMR 64x64, latent 32x32, near/far 1.2/4.0, 64 + 64, white background
+        sc = synth.scene_nmr(seed=3, n_rays=128)
+        save(*render_case("fw_cfg3_nmr", d_hidden=512, d_latent=512, seed=3, scene=sc,
+                          n_coarse=64, n_fine=64, n_fine_depth=0, white_bkgd=True, rng_seed=10,
+                          force_u_high=2))
+    if want("fw_cfg2_b128"):
+        # cfg2 on 128 rays of the frame (hashed pixels), a second weight / stream seed
+        sc = synth.scene_srn(seed=0, n_rays=128, pick="hash", theta_tgt=60.0)
+        save(*render_case("fw_cfg2_b128", d_hidden=512, d_latent=512, seed=7, scene=sc,
+                          n_coarse=64, n_fine=64, n_fine_depth=0, white_bkgd=True, rng_seed=11))
     if want("train_step"):
         save(*train_case("train_step"))
     if want("gen_rays"):

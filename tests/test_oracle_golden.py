@@ -12,7 +12,7 @@ import fixtures
 from oracle import ref_cpu
 
 RENDER_CASES = ["rw_ns1", "rw_lindisp", "rw_ns3_sb2", "rw_coarse_only",
-                "fw_cfg2", "fw_shipped", "fw_cfg1", "fw_dtu_ns3"]
+                "fw_cfg2", "fw_shipped", "fw_cfg1", "fw_dtu_ns3", "fw_cfg3_nmr", "fw_cfg2_b128"]
 ATOL = 1e-6
 
 
