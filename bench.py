@@ -1,41 +1,51 @@
 #!/usr/bin/env python
-"""Benchmark: pixelNeRF coarse + fine ray march (64 + 64 samples) on MI355X.
+"""Benchmark: pixelNeRF coarse + fine ray march (64 + 64 samples) on 1/2/4/8 MI355X.
 
-Workload (BASELINE.json configs[1], "cfg2"): SRN-cars 128x128 frame, 1 source
-view, rendered as 4096-ray chunks x (64 coarse + 64 fine), fp32.  One step =
-one full 128x128 frame (16,384 rays = 4 chunks) through
-``render_par(rays[None])`` exactly as eval/gen_video.py:213-217 drives it.
-Inputs are synthetic (hash-initialised MLP weights and latent) and
-already resident in HBM when the timed region starts.
-
-Multi-GPU (launched by torch.distributed.run): one process per GPU, every rank
-renders its own frame (a different target pose) — weak scaling, no data-path
-collective; a barrier + all_reduce(MAX) of the elapsed time bracket the region.
+Headline workload (`value`; BASELINE.json configs[2], SURVEY §8(d)/(e) "cfg3"): one
+ShapeNet-NMR batch of 24 target frames x 64x64 = 98,304 rays, 1 source view, 64 coarse +
+64 fine samples, STRONG scaling: the batch is fixed and each of the N ranks (one process
+per GPU) takes its contiguous ray range (pnr.dist.shard_range; the reference scatters rays
+the same way, nerf.py:367-371).  One step, per rank:
+  * encode the source image (the ResNet34 trunk, use_first_pool=False as
+    conf/exp/sn64.conf:4-8 sets it -> a 32x32 channels-last latent; models.py:89-144);
+  * the per-scene latent projection of both MLPs (lin_z folded into the latent,
+    pnr_latent_project) -- rebuilt every step, because the latent is new;
+  * render the rank's rays through ``render_par(rays[None])`` in gen_video.py's
+    ray_batch_size chunks of 50,000 (gen_video.py:213-217; args.py:19);
+  * copy the rank's rgb to the host (the launcher assembles the frames).
+No data-path collective: a barrier and an all_reduce(MAX) of the elapsed time bracket
+the timed region.  `value` = 98,304 x steps / max-over-ranks time, the same config at
+every N (N = 1 included), so the driver's SCALE runs compare with BENCH directly.
 
 The MLP arithmetic is --precision (default f16x3: fp32-accurate GEMMs from split-fp16
 products, include/pnr_abi.h); `dtype` stays "f32" (fp32 in / out / accumulation).
+Inputs are synthetic (hash-initialised MLP weights, random-init encoder, hashed source
+image), resident in HBM when the timed region starts.
 
 The JSON line also carries
-  roofline     — the dominant kernel (fine-pass fused point MLP, k_point_mlp):
-                 algorithmic fp32 FLOP per launch / its average duration measured with
-                 HIP events recorded on the launch stream inside the timed region,
-                 against the precision's fp32-equivalent MFMA peak (f16x3: 2500 / 3),
-                 plus the raw MFMA issue rate; `traffic` from the committed PMC pass;
-  composite    — the standalone alpha-composite kernel's HBM roofline (bytes per
-                 ray x rays / duration vs 8 TB/s) on a 1 M-ray batch;
-  extra_configs — cfg2 with the shipped conf, cfg3 (NMR 64x64) and cfg4 (DTU, 3 source
-                 views) on 1 GPU (informational; skip with --no-extra);
-  value_fp32_mfma — the same frame with the plain f32-MFMA arithmetic;
-  cpu_baseline — the CPU oracle (oracle/ref_cpu.py, a restatement of the
-                 reference's PyTorch path) on a bounded sample of the same frame,
-                 timed on this host, rank 0 at N = 1 only;
-  psnr_vs_reference_path — SURVEY §8(d)'s PSNR delta: the HIP render of that sample
-                 with the same injected random streams against the oracle's render.
+  roofline     -- the dominant kernel (fine-pass fused point MLP, k_point_mlp): its
+                  algorithmic FLOP per launch / its mean launch duration, both from HIP
+                  events recorded on the launch stream around every kernel inside the timed
+                  region; `traffic` from the committed rocprofv3 PMC pass;
+  train        -- cfg5 (BASELINE configs[4]): the training step (encoder, coarse + fine
+                  render, backward, bucketed RCCL gradient all-reduce, Adam), 4 x 256 rays
+                  per rank (weak scaling: 8 ranks = 8192 rays), at every N;
+  cfg2         -- (N = 1) BASELINE configs[1]: one SRN 128x128 frame as 4 x 4096-ray
+                  chunks, with its own roofline (the round-1 headline);
+  composite    -- (N = 1) the standalone alpha-composite kernel's HBM roofline;
+  extra_configs -- (N = 1) cfg2 with the shipped conf, mlp_fine=None, cfg4 (DTU, NS = 3);
+  cpu_baseline -- (N = 1, rank 0) the CPU oracle (oracle/ref_cpu.py) on a bounded sample
+                  of the headline batch, median of 3, plus cfg1 at full size and a cfg2
+                  subset, with os.cpu_count() and torch.get_num_threads() stated;
+  psnr_vs_reference_path -- SURVEY §8(d)'s PSNR delta: the HIP render of that sample with
+                  the same injected random streams against the oracle's render; fine-pass
+                  bin flips are proven from the coarse weights (oracle/parity.py).
 """
 import argparse
 import ctypes
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -54,7 +64,7 @@ from pnr.renderer import NeRFRenderer  # noqa: E402
 MFMA_F32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
 MFMA_BF16_PEAK_TFLOPS = 2500.0 # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
 # fp32-equivalent peak of each ResnetFC arithmetic mode (pnr.models.PRECISIONS): the
-# split modes issue 6 / 9 bf16 MFMA products per fp32 multiply-add
+# split modes issue 3 / 6 / 9 16-bit MFMA products per fp32 multiply-add
 PEAK_BY_PRECISION = {"fp32": (MFMA_F32_PEAK_TFLOPS, 1), "f16x3": (MFMA_BF16_PEAK_TFLOPS / 3, 3),
                      "bf16x6": (MFMA_BF16_PEAK_TFLOPS / 6, 6),
                      "bf16x9": (MFMA_BF16_PEAK_TFLOPS / 9, 9)}
@@ -73,18 +83,23 @@ FLOP_PER_POINT_NS1 = 4761600 + 2101248   # NS*4,761,600 + 2,101,2
 # FLOP the fused kernel executes per point with the projected latent (lin_z folded into the
 # latent per scene): lin_in + 5 blocks x (fc_0 + fc_1) + lin_out
 KERNEL_FLOP_PER_POINT_NS1 = 2 * 42 * 512 + 5 * 2 * 2 * 512 * 512 + 2 * 512 * 4   # 5,289,984
-PROJ_FLOP_PER_SCENE = 2 * 3 * 64 * 64 * 512 * 512   # 3 lin_z layers x 4096 latent pixels
 KC, KF = 64, 64
+# cfg3 (headline): ShapeNet-NMR 64x64, 24 target frames, latent 32x32
+NMR_SIZE, NMR_FRAMES, NMR_FOCAL, NMR_NEAR, NMR_FAR, NMR_RADIUS = 64, 24, 70.0, 1.2, 4.0, 2.7
+RAY_BATCH = 50000              # gen_video.py --ray_batch_size default (args.py:19)
+# cfg2: SRN 128x128 frame in 4096-ray chunks
 CHUNK = 4096
 W = H = 128
+KERNELS = ["sample_coarse", "mlp_coarse", "composite_coarse", "sample_fine", "mlp_fine", "composite_fine"]
 
 
-def model_conf():
+def model_conf(use_first_pool=True):
     mlp = dict(type="resnet", n_blocks=5, d_hidden=512, combine_layer=3, combine_type="average")
     return dict(use_encoder=True, use_xyz=True, use_code=True,
                 code=dict(num_freqs=6, freq_factor=1.5, include_input=True), use_viewdirs=True,
                 use_code_viewdirs=False, mlp_coarse=mlp, mlp_fine=mlp,
-                encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
+                encoder=dict(backbone="resnet34", pretrained=False, num_layers=4,
+                             use_first_pool=use_first_pool))
 
 
 class HipEvents:
@@ -95,7 +110,7 @@ class HipEvents:
         self.hip.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
         self.hip.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p,
                                                  ctypes.c_void_p]
-        self.hip.hipEventDestroy.argtypes = [ctypes.c_void_p]
+        self.hip.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 
     def create(self, n):
         evs = []
@@ -112,86 +127,279 @@ class HipEvents:
         return ms.value
 
 
-def build_scene(dev, rank):
-    sd = synth.pixelnerf_state(1)
-    net = PixelNeRFNet(model_conf())
-    net.load_state_dict(sd, strict=False)
+class RenderProbe:
+    """Records HIP events around every kernel of each fused render call while `on`
+    (pnr_render_forward_proj's `events` argument: no host synchronization is added), and
+    the call's ray count, so per-launch durations and algorithmic work come from the same
+    launches as the timed region."""
+
+    def __init__(self, ev):
+        self.ev = ev
+        self.lib = _lib.load()
+        self.orig = self.lib.pnr_render_forward_proj
+        self.on = False
+        self.calls = []      # (events, n_rays, n_coarse, n_fine)
+
+        def render_with_events(*a):
+            if not self.on:
+                return self.orig(*a)
+            evs = ev.create(7)
+            rays, cfg = a[6], a[8]
+            self.calls.append((evs, int(rays.n_rays), int(cfg.n_coarse), int(cfg.n_fine)))
+            arr = (ctypes.c_void_p * 7)(*[e.value for e in evs])
+            return self.orig(*a[:-1], arr)
+
+        self.lib.pnr_render_forward_proj = render_with_events
+
+    def reset(self):
+        self.calls = []
+
+    def summary(self, precision, latent_proj):
+        """Per-kernel mean ms, and the fine MLP's roofline over the recorded launches."""
+        per = {n: [] for n in KERNELS}
+        pts = []
+        for evs, n, kc, kf in self.calls:
+            for i, name in enumerate(KERNELS):
+                per[name].append(self.ev.elapsed_ms(evs[i], evs[i + 1]))
+            pts.append(n * (kc + kf))
+        avg = {k: sum(v) / len(v) for k, v in per.items() if v}
+        kflop = KERNEL_FLOP_PER_POINT_NS1 if latent_proj else FLOP_PER_POINT_NS1
+        pts_per_launch = sum(pts) / len(pts)
+        flop = pts_per_launch * kflop
+        ms = avg["mlp_fine"]
+        achieved = flop / (ms * 1e-3) / 1e12
+        peak, terms = PEAK_BY_PRECISION[precision]
+        kname = "k_point_mlp<%d, %s>" % (PRECISIONS[precision], "true" if latent_proj else "false")
+        return avg, {
+            "kernel": "k_point_mlp (fine pass)", "bound": "mfma",
+            "achieved": round(achieved, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s (fp32-equivalent: algorithmic FLOP per launch (%d FLOP per point x points "
+                    "per launch) / mean launch duration, HIP events on the launch stream)" % kflop,
+            "reference_equivalent_tflops": round(pts_per_launch * FLOP_PER_POINT_NS1 / (ms * 1e-3) / 1e12, 2),
+            "frac": round(achieved / peak, 4),
+            "mfma_issue": {"tflops": round(achieved * terms, 1),
+                           "peak": MFMA_F32_PEAK_TFLOPS if terms == 1 else MFMA_BF16_PEAK_TFLOPS,
+                           "products_per_fma": terms},
+            "points_per_launch": round(pts_per_launch, 1), "launches": len(pts),
+            "flop_per_launch": int(flop), "launch_ms": round(ms, 4),
+            "kernel_name": kname,
+        }
+
+
+def timed(fn, steps, warmup, dev, world):
+    """W untimed steps, then K timed steps between barrier + synchronize; max over ranks."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = fn()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    return pdist.max_over_ranks(t1 - t0, device=dev), res
+
+
+# ----------------------------------------------------------------- cfg3 --------------
+def nmr_inputs(dev):
+    """cfg3 inputs: a hashed 64x64 source image, its pose, and the 24-frame ray batch."""
+    img = torch.from_numpy(synth.hash_sym(31, (1, 3, NMR_SIZE, NMR_SIZE), 1.0)).to(dev)
+    src = synth.srn_poses([0.0], phi=-20.0, radius=NMR_RADIUS).to(dev)
+    tgt = synth.srn_poses([15.0 * i for i in range(NMR_FRAMES)], phi=-20.0, radius=NMR_RADIUS).to(dev)
+    focal = torch.tensor(NMR_FOCAL, device=dev)
+    rays = util.gen_rays(tgt, NMR_SIZE, NMR_SIZE, focal, NMR_NEAR, NMR_FAR).reshape(-1, 8).contiguous()
+    return img, src, focal, rays
+
+
+def make_net(dev, precision, latent_proj, use_first_pool=True):
+    torch.manual_seed(0)   # the random-init encoder is identical on every rank
+    net = PixelNeRFNet(model_conf(use_first_pool))
+    net.load_state_dict(synth.pixelnerf_state(1), strict=False)
     net = net.to(dev).eval()
-    lat = synth.latent(0, 1, 512, 64, 64).to(dev)
-    net.encode_latent(lat, synth.srn_poses([0.0]).to(dev), torch.tensor(131.25, device=dev), (W, H))
-    tgt = synth.srn_poses([30.0 + 15.0 * rank])
-    rays = util.gen_rays(tgt, W, H, torch.tensor(131.25), 0.01, 4.0).reshape(-1, 8).to(dev)
-    return sd, net, rays.contiguous()
+    net.mlp_precision = precision
+    net.use_latent_proj = latent_proj
+    return net
 
 
-def cpu_baseline(sd, rays_cpu, n_rays):
-    """Oracle (CPU restatement of the reference path) on a bounded sample."""
-    from oracle import ref_cpu
+def cfg3_leg(args, dev, rank, world, probe):
+    net = make_net(dev, args.precision, not args.no_latent_proj, use_first_pool=False)
+    img, src, focal, rays = nmr_inputs(dev)
+    n_all = rays.shape[0]
+    start, end = pdist.shard_range(n_all, rank, world)
+    mine = rays[start:end]
+    renderer = NeRFRenderer(n_coarse=KC, n_fine=KF, white_bkgd=True, eval_batch_size=RAY_BATCH).to(dev)
+    render_par = renderer.bind_parallel(net, simple_output=True).eval()
+    host = torch.empty(end - start, 3, pin_memory=True)
+    enc_ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
 
-    torch.set_num_threads(min(16, os.cpu_count() or 1))
-    scene = ref_cpu.Scene(synth.latent(0, 1, 512, 64, 64), synth.srn_poses([0.0]),
-                          torch.tensor(131.25), W, H, None)
-    rays = rays_cpu[:n_rays][None].contiguous()
-    streams = synth.rng_streams(2, n_rays, KC, KF, 0)
-    fn = lambda p, c, d: ref_cpu.pixelnerf_forward(sd, scene, p, c, d)  # noqa: E731
+    def step():
+        enc_ev[0].record()
+        net.encode(img, src, focal)          # ResNet34 trunk -> channels-last latent, cameras
+        enc_ev[1].record()
+        outs = [render_par(r[None])[0][0] for r in torch.split(mine, RAY_BATCH, dim=0)]
+        rgb = torch.cat(outs)
+        host.copy_(rgb, non_blocking=True)   # the rank's shard lands in host memory
+        return rgb
+
+    torch.backends.cudnn.benchmark = True
+    torch.manual_seed(1234 + rank)
     with torch.no_grad():
-        ref_cpu.render(fn, rays[:, :8], KC, KF, 0, tuple(s[:8] for s in streams), True)  # warm-up
-        t0 = time.perf_counter()
-        ref = ref_cpu.render(fn, rays, KC, KF, 0, streams, True)
-        dt = time.perf_counter() - t0
-    return dict(value=round(n_rays / dt, 2), unit="rays/s", cores=torch.get_num_threads(),
-                kind="port",
-                sample="%d rays of the cfg2 frame x (64+64) samples, oracle/ref_cpu.py, %.1f s" % (
-                    n_rays, dt)), ref, streams
+        for _ in range(args.warmup):
+            step()
+        probe.reset()
+        probe.on = True
+        elapsed, rgb = timed(step, args.steps, 0, dev, world)
+        probe.on = False
+    assert bool(torch.isfinite(rgb).all())
+    avg, roof = probe.summary(args.precision, net.use_latent_proj)
+    enc = enc_ev[0].elapsed_time(enc_ev[1])   # the last timed step's encode
+    return net, (img, src, focal, rays), elapsed, avg, roof, enc, (start, end)
 
 
-def psnr_vs_reference_path(net, rays_dev, ref, streams, dev):
-    """SURVEY §8(d)'s PSNR delta: the HIP render of the cpu_baseline rays with the SAME
-    injected random streams, against the oracle's render of them (oracle/ref_cpu.py, the
-    CPU restatement pinned to the reference).  `agreement_db` = PSNR(HIP, oracle);
-    `delta_db` = PSNR(HIP, target) - PSNR(oracle, target) for a seeded U(0,1) target image
-    (no ground-truth frames offline).  Fine-pass rays are excluded from the `_excl_flips`
-    figures only for a searchsorted bin flip PROVEN from the two sets of coarse weights
-    (oracle/parity.py); `unexplained_rays` (fine samples that differ without one) must be 0."""
-    from oracle import parity
+# ----------------------------------------------------------------- cfg2 --------------
+def cfg2_leg(args, dev, probe):
+    """BASELINE configs[1]: one SRN 128x128 frame, 4 x 4096-ray chunks (N = 1)."""
+    net = make_net(dev, args.precision, not args.no_latent_proj)
+    net.encode_latent(synth.latent(0, 1, 512, 64, 64).to(dev), synth.srn_poses([0.0]).to(dev),
+                      torch.tensor(131.25, device=dev), (W, H))
+    rays = util.gen_rays(synth.srn_poses([30.0]).to(dev), W, H, torch.tensor(131.25), 0.01, 4.0)
+    chunks = list(torch.split(rays.reshape(-1, 8).contiguous(), CHUNK, dim=0))
+    renderer = NeRFRenderer(n_coarse=KC, n_fine=KF, white_bkgd=True, eval_batch_size=CHUNK).to(dev)
+    render_par = renderer.bind_parallel(net, simple_output=True).eval()
 
-    n = rays_dev.shape[0]
-    r = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True).to(dev)
-    r.streams = tuple(t.to(dev) for t in streams)
-    r.return_z = True
+    def step():
+        net.drop_latent_proj()   # per-scene projection rebuilt inside every timed frame
+        return torch.cat([render_par(r[None])[0][0] for r in chunks])
+
     with torch.no_grad():
-        out = r(net, rays_dev[None].contiguous(), want_weights=True)
-    tgt = torch.from_numpy(synth.hash_uniform(5, n * 3).astype("float32")).reshape(n, 3)
-    cls = parity.classify_fine(out.coarse.weights[0], ref["coarse"]["weights"][0], streams[1],
-                               out.fine.z[0], ref["fine"]["z"])
-
-    def psnr(a, b):   # util.psnr (util.py:474-481), +inf for identical images
-        return float("inf") if float(((a - b) ** 2).mean()) == 0.0 else float(util.psnr(a, b))
-
-    res = {}
-    for name in ("coarse", "fine"):
-        mine = getattr(out, name).rgb[0].float().cpu()
-        theirs = ref[name]["rgb"][0].float()
-        agree = psnr(mine, theirs)
-        flip = cls["flip"] if name == "fine" else torch.zeros(n, dtype=torch.bool)
-        keep = ~flip
-        agree_kept = psnr(mine[keep], theirs[keep]) if bool(keep.any()) else float("inf")
-        d = (mine - theirs).abs()
-        res[name] = dict(agreement_db=round(agree, 2) if agree < float("inf") else None,
-                         delta_db=round(psnr(mine, tgt) - psnr(theirs, tgt), 6),
-                         max_abs_rgb=float(d.max()),
-                         bin_flip_rays=int(flip.sum()),
-                         agreement_db_excl_flips=round(agree_kept, 2) if agree_kept < float("inf") else None,
-                         max_abs_rgb_excl_flips=float(d[keep].max()) if bool(keep.any()) else 0.0,
-                         rays_outside_tol_excl_flips=int(((d > 5e-5 + 1e-5 * theirs.abs()).any(-1) & keep).sum()))
-    res["fine"]["flip_rays"] = cls["flip_idx"][:16]
-    res["fine"]["unexplained_rays"] = int(cls["unexplained"].sum())
-    res["rays"] = n
-    res["flip_rule"] = ("fine-bin flip = searchsorted bins recomputed from the HIP and the oracle "
-                        "coarse weights with the same u differ (oracle/parity.py)")
-    return res
+        for _ in range(args.warmup):
+            step()
+        probe.reset()
+        probe.on = True
+        elapsed, img = timed(step, args.steps, 0, dev, 1)
+        probe.on = False
+        value_fp32 = None
+        if args.precision != "fp32" and not args.no_compare:
+            net.mlp_precision = "fp32"
+            t_fp32, _ = timed(step, 2, 1, dev, 1)
+            value_fp32 = round(2 * W * H / t_fp32, 1)
+            net.mlp_precision = args.precision
+    assert bool(torch.isfinite(img).all())
+    avg, roof = probe.summary(args.precision, net.use_latent_proj)
+    return dict(value=round(W * H * args.steps / elapsed, 1), unit="rays/s",
+                ms_per_frame=round(1e3 * elapsed / args.steps, 3),
+                workload="cfg2: SRN-cars 128x128 frame, 1 source view, 4096-ray chunks x (64 + 64)",
+                roofline=roof, kernel_ms={k: round(v, 4) for k, v in avg.items()},
+                value_fp32_mfma=value_fp32,
+                l2_stream=l2_stream(roof["points_per_launch"], roof["launch_ms"], args.precision,
+                                    net.use_latent_proj))
 
 
+# ----------------------------------------------------------------- cfg5 --------------
+def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256, ns=1, graph=False,
+              sync_debug=False):
+    """cfg5 (BASELINE configs[4]; the reference's train.py:182-283) on synthetic SRN-shaped
+    data: encode SB x NS source images (ResNet34 trunk), render SB x B' rays with the shipped
+    conf (64 coarse + 32 fine incl. 16 depth, white background) through the HIP training path
+    (pnr/train.py), MSE(coarse) + MSE(fine) (conf/default.conf:77-78), backward, bucketed
+    gradient mean over RCCL/xGMI (pnr.dist.allreduce_grads), Adam lr 1e-4 (trainer.py:49).
+    Weak scaling: SB x B' rays per rank.  Returns the result dict (max-over-ranks timing)."""
+    from pnr.models import make_model
+
+    torch.manual_seed(1234 + rank)
+    torch.backends.cudnn.benchmark = True   # MIOpen solver search for the encoder convolutions
+    net = make_model(model_conf()).to(dev)
+    net.load_state_dict(synth.pixelnerf_state(0), strict=False)
+    net.mlp_precision = precision
+    net.train()
+    renderer = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(dev)
+    # fused Adam: one multi-tensor kernel per step (the reference uses torch.optim.Adam, same update);
+    # capturable keeps the step counter on the device so the update replays inside a graph
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=graph)
+    params = list(net.parameters())
+    focal = torch.tensor(131.25, device=dev)
+    src_poses = synth.srn_poses([float(15 * i + 7 * rank + 40 * v) for i in range(sb) for v in range(ns)]).to(dev)
+    if ns > 1:
+        src_poses = src_poses.reshape(sb, ns, 4, 4)
+    tgt_poses = synth.srn_poses([float(15 * i + 7 * rank + 90) for i in range(sb)]).to(dev)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    images = (torch.rand(sb, 3, H, W, device=dev, generator=g) * 2 - 1 if ns == 1 else
+              torch.rand(sb, ns, 3, H, W, device=dev, generator=g) * 2 - 1)
+    all_rays = util.gen_rays(tgt_poses, W, H, focal, 0.8, 1.8).reshape(sb, -1, 8)   # on device
+    pix = torch.randint(0, W * H, (sb, per), device=dev, generator=g)
+    rays = torch.gather(all_rays, 1, pix[..., None].expand(-1, -1, 8)).contiguous()
+    target = torch.rand(sb, per, 3, device=dev, generator=g)
+    mse = torch.nn.functional.mse_loss
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        net.encode(images, src_poses, focal)
+        out = renderer(net, rays, want_weights=True)
+        loss = mse(out.coarse.rgb, target) + mse(out.fine.rgb, target)
+        loss.backward()
+        pdist.allreduce_grads(params, world)
+        opt.step()
+        return loss
+
+    run = step
+    if graph:
+        # HIP graph of the whole step: warm-up on a side stream (MIOpen solver search, pack
+        # caches, allocator), then capture; inputs are static tensors
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(max(warmup, 2)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        cg = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(cg):
+            static_loss = step()
+
+        def run():
+            cg.replay()
+            return static_loss
+
+        warmup = 1
+    for _ in range(warmup):
+        run()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    if sync_debug:
+        torch.cuda.set_sync_debug_mode("warn")
+    for _ in range(steps):
+        loss = run()
+    if sync_debug:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = pdist.max_over_ranks(t1 - t0, dev)
+    rays_total = sb * per * steps * world
+    arith = (precision + " forward + f16x3 fused input-gradient chain + split-bf16 (x6) weight gradients"
+             if precision == "f16x3" and ns == 1 else
+             precision + " forward + fp32 GEMM input-gradient chain + split-bf16 (x6) weight gradients"
+             if precision == "f16x3" else precision + " forward, fp32 GEMM backward")
+    return {
+        "metric": "training rays/sec (cfg5: encoder + coarse/fine render + backward + grad all-reduce + Adam)",
+        "value": round(rays_total / elapsed, 1), "unit": "rays/s", "n_gpus": world, "steps": steps,
+        "ms_per_step": round(elapsed / steps * 1e3, 3), "scaling": "weak",
+        "arithmetic": arith + " (pnr/train.py)",
+        "config": {"workload": "cfg5: SB=%d objects x %d rays per rank, %d source view(s), 64 coarse + 32 fine "
+                               "(16 depth)" % (sb, per, ns), "global_batch_rays": sb * per * world,
+                   "parallelism": "data parallel, 1 process per GPU, bucketed RCCL all-reduce (32 MB buckets)",
+                   "launch": "one HIP graph per step" if graph else "eager"},
+        "loss": round(float(loss.item()), 6),
+    }
+
+
+# ----------------------------------------------------------------- roofline helpers --
 def composite_roofline(dev, ev):
     """Standalone composite kernel on 1 M rays x 128 samples (HBM-bound)."""
     from pnr import ops
@@ -251,10 +459,10 @@ def _time_render(net, renderer, rays, chunk, passes=2):
 
 
 def extra_configs(dev, precision, latent_proj=True):
-    """The other SURVEY §8(d) workloads on 1 GPU (informational, not `value`):
-    cfg2 with the shipped conf (64 + 32 incl. 16 depth samples), cfg3 NMR 64x64 (latent
-    32x32, 24 frames x 4096 rays), cfg4 DTU 400x300 with NS = 3 source views (one 120,000-
-    ray frame, the multi-view mean path), chunked as gen_video.py does (50,000 rays)."""
+    """Other SURVEY §8(d) workloads on 1 GPU (informational, not `value`): cfg2 with the
+    shipped conf (64 + 32 incl. 16 depth samples), cfg2 as eval_approx.py --coarse renders it
+    (mlp_fine = None, 64 + 128), cfg4 DTU 400x300 with NS = 3 source views (one 120,000-ray
+    frame, the multi-view mean path) in gen_video's 50,000-ray chunks."""
     res = {}
     sd = synth.pixelnerf_state(1)
 
@@ -268,36 +476,24 @@ def extra_configs(dev, precision, latent_proj=True):
                           c=c.to(dev) if c is not None else None, num_objs=n_obj)
         return net
 
-    # cfg2, shipped renderer conf
     net = make(synth.latent(0, 1, 512, 64, 64), synth.srn_poses([0.0]), torch.tensor(131.25), (W, H))
     rays = util.gen_rays(synth.srn_poses([30.0]).to(dev), W, H, torch.tensor(131.25), 0.01, 4.0).reshape(-1, 8)
     r = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(dev)
     s = _time_render(net, r, rays, CHUNK)
     res["cfg2_shipped_64_32_16"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
                                         gflop_per_ray=round(160 * FLOP_PER_POINT_NS1 / 1e9, 4))
-    # cfg2 as eval_approx.py --coarse renders it: mlp_fine = None, 64 + 128 samples (the fine
-    # pass reuses the coarse pass's outputs for the 64 coarse samples)
     net.mlp_fine = None
     r = NeRFRenderer(n_coarse=64, n_fine=128, white_bkgd=True).to(dev)
     s = _time_render(net, r, rays, CHUNK)
     res["cfg2_coarse_as_fine_64_128"] = dict(rays_per_s=round(rays.shape[0] / s, 1),
                                              ms_per_frame=round(s * 1e3, 3))
-    # cfg3, NMR 64x64: 24 target views of one object
-    net = make(synth.latent(3, 1, 512, 32, 32), synth.srn_poses([0.0], radius=2.7), torch.tensor(70.0), (64, 64))
-    rays = util.gen_rays(synth.srn_poses([15.0 * i for i in range(24)], radius=2.7).to(dev), 64, 64,
-                         torch.tensor(70.0), 1.2, 4.0).reshape(-1, 8)
-    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True).to(dev)
-    s = _time_render(net, r, rays, 16384)
-    res["cfg3_nmr64_24frames"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_batch=round(s * 1e3, 3),
-                                      rays=int(rays.shape[0]))
-    # cfg4, DTU 400x300, 3 source views
     sc = synth.scene_multiview(seed=8, n_views=3, n_rays=1)
     net = make(synth.latent(8, 3, 512, 150, 200), sc["poses"][None], sc["focal"][None], (400, 300),
                c=sc["c"][None])
     rays = util.gen_rays(synth.srn_poses([10.0], phi=-12.0, radius=2.0).to(dev), 400, 300, sc["focal"],
                          0.1, 5.0, c=sc["c"]).reshape(-1, 8)
     r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=False).to(dev)
-    s = _time_render(net, r, rays, 50000, passes=1)
+    s = _time_render(net, r, rays, RAY_BATCH, passes=1)
     res["cfg4_dtu_ns3_frame"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
                                      gflop_per_ray=round(192 * (3 * 4761600 + 2101248) / 1e9, 4))
     return res
@@ -315,7 +511,7 @@ def l2_stream(points, launch_ms, precision, latent_proj):
     against the guide's aggregate L2 rate (and, for scale, its measured gather-loop rate)."""
     if precision != "f16x3":
         return None
-    tiles = (points + 63) // 64
+    tiles = int((points + 63) // 64)
     # packed 512x512 layers (10, or 13 with the per-point lin_z GEMMs), lin_in, lin_out
     weights = (10 if latent_proj else 13) * (1 << 20) + (128 << 10) + (32 << 10)
     gather = 3 * 64 * 4 * 2048   # 3 blends x 64 points x 4 corners x 2 KB rows (P or the latent)
@@ -324,42 +520,148 @@ def l2_stream(points, launch_ms, precision, latent_proj):
     return {"kernel": "k_point_mlp (fine pass)", "bytes_per_tile": weights + gather, "tiles": tiles,
             "achieved": round(tbs, 2), "peak": L2_PEAK_TBS, "unit": "TB/s (L2 -> CU)",
             "frac": round(tbs / L2_PEAK_TBS, 4),
-            "frac_of_gather_loop": round(tbs / L2_GATHER_LOOP_TBS, 4),
-            "note": "packed weight fragments per 64-point tile + 4-corner latent rows; peak is the "
-                    "guide's aggregate L2 figure; frac_of_gather_loop compares with its measured "
-                    "L2 gather loop (16.8-18.8 TB/s at <= 72 KiB in flight per CU)"}
+            "frac_of_gather_loop": round(tbs / L2_GATHER_LOOP_TBS, 4)}
 
 
-def pmc_traffic(kernel, render_pass):
-    """Mean HBM bytes per launch of `kernel` in `render_pass` ("fine" / "coarse") from the
-    newest committed PMC summary that has it (rocprofv3 counters cannot be read live from
-    inside the process).  Returns (bytes, summary path) or (None, None)."""
+def pmc_traffic(kernel, render_pass, workload):
+    """Mean HBM bytes per launch of `kernel` in `render_pass` of `workload` from the newest
+    committed PMC summary that has it (rocprofv3 counters cannot be read live from inside
+    the process).  Returns (bytes, summary path) or (None, None)."""
     import csv
     import glob
 
     for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")), reverse=True):
         vals = []
         with open(path) as fh:
-            rows = [f for f in csv.reader(l for l in fh if not l.startswith("#") and not l.startswith("kernel,"))]
+            rows = list(csv.reader(ln for ln in fh if not ln.startswith("#") and not ln.startswith("kernel,")))
         for f in rows:   # kernel names are quoted (they contain commas: k_point_mlp<3, true>)
-            if f and f[0].endswith(kernel) and len(f) > 6 and f[6] == render_pass:
+            if f and f[0].endswith(kernel) and len(f) > 7 and f[6] == render_pass and f[7] == workload:
                 vals.append(int(f[5]))
         if vals:
             return sum(vals) // len(vals), os.path.relpath(path, REPO)
     return None, None
 
 
+# ----------------------------------------------------------------- CPU baseline -----
+def cpu_baselines(sd, nmr, net3, dev, n_rays):
+    """The oracle (oracle/ref_cpu.py, the CPU restatement of the reference path, pinned to
+    the reference's outputs) on the box's host cores, median of 3 after a warm-up:
+      * the headline's bounded sample: n_rays rays spread evenly over the cfg3 batch x (64+64),
+        on the latent the GPU leg's encoder produced;
+      * cfg1 at full size (256 rays x 32 coarse samples; BASELINE configs[0]);
+      * cfg2 on a 512-ray subset of the 128x128 frame x (64+64), extrapolated per ray.
+    Returns (baseline dict, oracle render of the cfg3 sample, its ray indices, its streams)."""
+    from oracle import ref_cpu
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+
+    def median_run(fn):
+        fn(warm=True)
+        times, out = [], None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            out = fn(warm=False)
+            times.append(time.perf_counter() - t0)
+        return statistics.median(times), times, out
+
+    def runner(scene, rays, streams, kc, kf):
+        def run(warm):
+            rr, ss = (rays[:8], tuple(s[:8] for s in streams)) if warm else (rays, streams)
+            with torch.no_grad():
+                return ref_cpu.render(lambda p, c, d: ref_cpu.pixelnerf_forward(sd, scene, p, c, d),
+                                      rr[None], kc, kf, 0, ss, True)
+        return run
+
+    img, src, focal, rays3 = nmr
+    idx = torch.linspace(0, rays3.shape[0] - 1, n_rays).round().long().to(dev)
+    scene3 = ref_cpu.Scene(net3.encoder.latent.detach().float().cpu().contiguous(), src.cpu(),
+                           torch.tensor(NMR_FOCAL), NMR_SIZE, NMR_SIZE, None)
+    st3 = synth.rng_streams(2, n_rays, KC, KF, 0)
+    t3, runs3, ref3 = median_run(runner(scene3, rays3[idx].cpu(), st3, KC, KF))
+    sc1 = synth.scene_srn(seed=0, n_rays=256)
+    scene1 = ref_cpu.Scene(sc1["latent"], sc1["poses"], sc1["focal"], W, H, None)
+    t1, runs1, _ = median_run(runner(scene1, sc1["rays"], synth.rng_streams(9, 256, 32, 0, 0), 32, 0))
+    sc2 = synth.scene_srn(seed=0, n_rays=512, pick="hash")
+    scene2 = ref_cpu.Scene(sc2["latent"], sc2["poses"], sc2["focal"], W, H, None)
+    t2, runs2, _ = median_run(runner(scene2, sc2["rays"], synth.rng_streams(3, 512, KC, KF, 0), KC, KF))
+    fmt = lambda ts: ", ".join("%.2f" % t for t in ts)  # noqa: E731
+    base = dict(value=round(n_rays / t3, 2), unit="rays/s", cores=torch.get_num_threads(), kind="port",
+                os_cpu_count=os.cpu_count(), torch_num_threads=torch.get_num_threads(),
+                sample="%d rays spread evenly over the cfg3 98,304-ray batch x (64+64) samples, "
+                       "oracle/ref_cpu.py, median of 3 runs (%s s)" % (n_rays, fmt(runs3)),
+                cfg1_full=dict(value=round(256 / t1, 2), unit="rays/s",
+                               sample="cfg1 at full size: 256 rays x 32 coarse, median of 3 (%s s)" % fmt(runs1)),
+                cfg2_subset=dict(value=round(512 / t2, 2), unit="rays/s",
+                                 sample="cfg2: 512 hashed rays of the 128x128 frame x (64+64), median of 3 "
+                                        "(%s s), extrapolated per ray" % fmt(runs2)))
+    return base, ref3, idx, st3
+
+
+def psnr_vs_reference_path(net, rays_dev, ref, streams, dev):
+    """SURVEY §8(d)'s PSNR delta: the HIP render of the cpu_baseline rays with the SAME
+    injected random streams, against the oracle's render of them (oracle/ref_cpu.py, the
+    CPU restatement pinned to the reference).  `agreement_db` = PSNR(HIP, oracle);
+    `delta_db` = PSNR(HIP, target) - PSNR(oracle, target) for a seeded U(0,1) target image
+    (no ground-truth frames offline).  Fine-pass rays are excluded from the `_excl_flips`
+    figures only for a searchsorted bin flip PROVEN from the two sets of coarse weights
+    (oracle/parity.py); `unexplained_rays` (fine samples that differ without one) must be 0."""
+    from oracle import parity
+
+    n = rays_dev.shape[0]
+    r = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True).to(dev)
+    r.streams = tuple(t.to(dev) for t in streams)
+    r.return_z = True
+    with torch.no_grad():
+        out = r(net, rays_dev[None].contiguous(), want_weights=True)
+    tgt = torch.from_numpy(synth.hash_uniform(5, n * 3).astype("float32")).reshape(n, 3)
+    z_exp = parity.expected_fine_z(rays_dev, out.coarse.z, out.coarse.weights, out.coarse.depth, streams,
+                                   KC, KF, 0)
+    cls = parity.classify_fine(out.coarse.weights[0], ref["coarse"]["weights"][0], streams[1],
+                               out.fine.z[0], ref["fine"]["z"], z_exp)
+
+    def psnr(a, b):   # util.psnr (util.py:474-481), +inf for identical images
+        return float("inf") if float(((a - b) ** 2).mean()) == 0.0 else float(util.psnr(a, b))
+
+    res = {}
+    for name in ("coarse", "fine"):
+        mine = getattr(out, name).rgb[0].float().cpu()
+        theirs = ref[name]["rgb"][0].float()
+        agree = psnr(mine, theirs)
+        flip = cls["flip"] if name == "fine" else torch.zeros(n, dtype=torch.bool)
+        keep = ~flip
+        agree_kept = psnr(mine[keep], theirs[keep]) if bool(keep.any()) else float("inf")
+        d = (mine - theirs).abs()
+        res[name] = dict(agreement_db=round(agree, 2) if agree < float("inf") else None,
+                         delta_db=round(psnr(mine, tgt) - psnr(theirs, tgt), 6),
+                         max_abs_rgb=float(d.max()),
+                         bin_flip_rays=int(flip.sum()),
+                         agreement_db_excl_flips=round(agree_kept, 2) if agree_kept < float("inf") else None,
+                         max_abs_rgb_excl_flips=float(d[keep].max()) if bool(keep.any()) else 0.0,
+                         rays_outside_tol_excl_flips=int(((d > 5e-5 + 1e-5 * theirs.abs()).any(-1) & keep).sum()))
+    res["fine"]["flip_rays"] = cls["flip_idx"][:16]
+    res["fine"]["unexplained_rays"] = int(cls["unexplained"].sum())
+    res["fine"]["flips_not_following_own_coarse_weights"] = int(cls["inconsistent"].sum())
+    res["rays"] = n
+    res["flip_rule"] = ("fine-bin flip = searchsorted bins recomputed from the HIP and the oracle "
+                        "coarse weights with the same u differ (oracle/parity.py)")
+    return res
+
+
+# ----------------------------------------------------------------- main --------------
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cpu-rays", type=int, default=4096)   # ~13 s of oracle work on 16 cores
+    ap.add_argument("--cpu-rays", type=int, default=512, help="oracle sample of the headline batch")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-composite", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the cfg2-shipped / cfg3 / cfg4 lines")
-    ap.add_argument("--no-compare", action="store_true",
-                    help="skip the f32-MFMA comparison frame (profiling runs)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the cfg2-shipped / coarse-as-fine / cfg4 lines")
+    ap.add_argument("--no-cfg2", action="store_true", help="skip the cfg2 frame leg")
+    ap.add_argument("--no-train", action="store_true", help="skip the cfg5 training leg")
+    ap.add_argument("--no-compare", action="store_true", help="skip the f32-MFMA comparison frame")
+    ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
     ap.add_argument("--no-latent-proj", action="store_true",
                     help="per-point lin_z GEMMs on the gathered latent (A/B against the projection)")
@@ -368,144 +670,57 @@ def main():
     rank, world, local = pdist.init_from_env("nccl")   # RCCL on ROCm; control plane only
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    sd, net, rays = build_scene(dev, rank)
-    net.mlp_precision = args.precision
-    net.use_latent_proj = not args.no_latent_proj
-    renderer = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True,
-                            eval_batch_size=CHUNK).to(dev)
-    render_par = renderer.bind_parallel(net, [local], simple_output=True).eval()
-    lib = _lib.load()
-    chunks = list(torch.split(rays, CHUNK, dim=0))
     ev = HipEvents()
+    probe = RenderProbe(ev)
 
-    # instrument the fused render: record events around every kernel of each chunk
-    orig = lib.pnr_render_forward_proj
-    pool = []
-    recording = {"on": False}
-
-    def render_with_events(*a):
-        if not recording["on"]:
-            return orig(*a)
-        evs = ev.create(7)
-        pool.append(evs)
-        arr = (ctypes.c_void_p * 7)(*[e.value for e in evs])
-        return orig(*a[:-1], arr)
-
-    lib.pnr_render_forward_proj = render_with_events
-
-    def step():
-        # the per-scene latent projection (lin_z folded into the latent) is rebuilt inside
-        # every timed frame: nothing beyond the encoder latent is carried across steps
-        net.drop_latent_proj()
-        frame = []
-        for r in chunks:
-            rgb, _depth = render_par(r[None])
-            frame.append(rgb[0])
-        return torch.cat(frame)
-
-    torch.manual_seed(1234 + rank)
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        recording["on"] = True
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            img = step()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        recording["on"] = False
-        if world > 1:
-            dist.barrier()
-    elapsed = pdist.max_over_ranks(t1 - t0, device=dev)
-    assert bool(torch.isfinite(img).all())
-
-    # per-kernel durations from the events recorded in the timed region
-    names = ["sample_coarse", "mlp_coarse", "composite_coarse", "sample_fine", "mlp_fine",
-             "composite_fine"]
-    per = {n: [] for n in names}
-    for evs in pool:
-        for i, n in enumerate(names):
-            per[n].append(ev.elapsed_ms(evs[i], evs[i + 1]))
-    avg = {n: sum(v) / len(v) for n, v in per.items()}
-    pts_fine = CHUNK * (KC + KF)
-    kflop = KERNEL_FLOP_PER_POINT_NS1 if net.use_latent_proj else FLOP_PER_POINT_NS1
-    flop_fine = pts_fine * kflop
-    achieved = flop_fine / (avg["mlp_fine"] * 1e-3) / 1e12
-    ref_equiv = pts_fine * FLOP_PER_POINT_NS1 / (avg["mlp_fine"] * 1e-3) / 1e12
-    peak, terms = PEAK_BY_PRECISION[args.precision]
-
-    # same frame with the plain f32-MFMA arithmetic, for comparison (N = 1 only)
-    value_fp32 = None
-    if world == 1 and args.precision != "fp32" and not args.no_compare:
-        net.mlp_precision = "fp32"
-        with torch.no_grad():
-            step()
-            torch.cuda.synchronize(dev)
-            t2 = time.perf_counter()
-            for _ in range(2):
-                step()
-            torch.cuda.synchronize(dev)
-            value_fp32 = round(2 * W * H / (time.perf_counter() - t2), 1)
-        net.mlp_precision = args.precision
-
-    prec_code = PRECISIONS[args.precision]
-    kname = "k_point_mlp<%d, %s>" % (prec_code, "true" if net.use_latent_proj else "false")
-    traffic, traffic_src = pmc_traffic(kname, "fine")
-    rays_total = W * H * args.steps * world
-    value = rays_total / elapsed
+    net3, nmr, elapsed, avg, roof, enc_ms, (start, end) = cfg3_leg(args, dev, rank, world, probe)
+    n_batch = nmr[3].shape[0]
+    traffic, traffic_src = pmc_traffic(roof["kernel_name"], "fine", "cfg3")
+    roof["traffic"] = traffic
+    roof["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, fine-pass "
+                              "launches of %s (%s, FETCH x2 gfx950 correction)" % (roof["kernel_name"], traffic_src))
     out = {
         "metric": "rays/sec (coarse+fine, 64+64 samples)",
-        "value": round(value, 1),
+        "value": round(n_batch * args.steps / elapsed, 1),
         "unit": "rays/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f32",
         "arithmetic": ARITHMETIC[args.precision],
-        "value_fp32_mfma": value_fp32,
-        "data": "synthetic (hash-initialised ResnetFC weights + latent; SRN geometry)",
-        "config": {"workload": "cfg2: SRN-cars 128x128 frame, 1 source view, 4096-ray chunks x "
-                               "(64 coarse + 64 fine)", "frame": [W, H], "chunk_rays": CHUNK,
-                   "n_coarse": KC, "n_fine": KF, "n_views": 1, "rays_per_step_per_gpu": W * H,
-                   "parallelism": "rays sharded by frame, 1 process per GPU"},
-        "latent_proj": {"on": bool(net.use_latent_proj),
-                        "flop_per_scene_per_mlp": PROJ_FLOP_PER_SCENE,
-                        "note": "lin_z of every latent pixel (pnr_latent_project), rebuilt for both "
-                                "MLPs inside every timed step; the kernel blends 4 projected rows per "
-                                "point instead of 3 per-point 512x512 lin_z GEMMs"},
-        "roofline": {"kernel": "k_point_mlp (fine pass)", "bound": "mfma",
-                     "achieved": round(achieved, 2), "peak": round(peak, 1),
-                     "unit": "TFLOP/s (fp32-equivalent: the kernel's algorithmic FLOP per launch / "
-                             "launch time; %d FLOP per point)" % kflop,
-                     "reference_equivalent_tflops": round(ref_equiv, 2),
-                     "frac": round(achieved / peak, 4),
-                     "mfma_issue": {"tflops": round(achieved * terms, 1),
-                                    "peak": MFMA_F32_PEAK_TFLOPS if terms == 1 else MFMA_BF16_PEAK_TFLOPS,
-                                    "products_per_fma": terms},
-                     "traffic": traffic,
-                     "traffic_source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this "
-                                       "bench, fine-pass launches of %s (%s, FETCH x2 "
-                                       "gfx950 correction)" % (kname, traffic_src),
-                     "flop_per_launch": flop_fine,
-                     "launch_ms": round(avg["mlp_fine"], 4)},
-        "kernel_ms": {n: round(v, 4) for n, v in avg.items()},
-        "l2_stream": l2_stream(pts_fine, avg["mlp_fine"], args.precision, net.use_latent_proj),
+        "data": "synthetic (hash-initialised ResnetFC weights, random-init ResNet34 encoder on a hashed "
+                "64x64 source image; NMR geometry)",
+        "config": {"workload": "cfg3: ShapeNet-NMR 64x64, 1 source view, 24 frames = 98,304 rays per step "
+                               "x (64 coarse + 64 fine), ray-batch sharded over the GPUs",
+                   "frames": NMR_FRAMES, "frame": [NMR_SIZE, NMR_SIZE], "rays_per_step": n_batch,
+                   "rays_rank0": end - start if rank == 0 else None, "ray_batch_size": RAY_BATCH,
+                   "n_coarse": KC, "n_fine": KF, "n_views": 1, "latent": [32, 32],
+                   "near_far": [NMR_NEAR, NMR_FAR], "focal": NMR_FOCAL,
+                   "parallelism": "contiguous ray ranges, 1 process per GPU, no data-path collective",
+                   "per_step": "encode (ResNet34) + latent projection + render + device->host copy"},
+        "encode_ms": round(enc_ms, 3),
+        "roofline": roof,
+        "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
+        "l2_stream": l2_stream(roof["points_per_launch"], roof["launch_ms"], args.precision,
+                               not args.no_latent_proj),
     }
-    if rank == 0 and world == 1 and not args.no_composite:
-        out["composite"] = composite_roofline(dev, ev)
-    if rank == 0 and world == 1 and not args.no_extra:
-        out["extra_configs"] = extra_configs(dev, args.precision, not args.no_latent_proj)
-    if rank == 0 and world == 1 and not args.no_cpu:
-        out["cpu_baseline"], ref, streams = cpu_baseline(sd, rays.cpu(), args.cpu_rays)
-        out["psnr_vs_reference_path"] = psnr_vs_reference_path(net, rays[:args.cpu_rays], ref, streams, dev)
+    if not args.no_train:
+        out["train"] = train_leg(dev, rank, world, args.train_steps, 2, precision=args.precision)
+    if rank == 0 and world == 1:
+        if not args.no_cfg2:
+            out["cfg2"] = cfg2_leg(args, dev, probe)
+        if not args.no_composite:
+            out["composite"] = composite_roofline(dev, ev)
+        if not args.no_extra:
+            out["extra_configs"] = extra_configs(dev, args.precision, not args.no_latent_proj)
+        if not args.no_cpu:
+            sd = synth.pixelnerf_state(1)
+            out["cpu_baseline"], ref, idx, streams = cpu_baselines(sd, nmr, net3, dev, args.cpu_rays)
+            out["psnr_vs_reference_path"] = psnr_vs_reference_path(net3, nmr[3][idx], ref, streams, dev)
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

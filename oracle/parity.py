@@ -54,7 +54,29 @@ def close_mask(a, b, atol=ATOL, rtol=RTOL):
     return (a - b).abs() <= atol + rtol * b.abs()
 
 
-def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref):
+def expected_fine_z(rays, z_coarse, w_coarse, depth_coarse, streams, n_coarse, n_fine, n_fine_depth,
+                    depth_std=0.01, lindisp=False):
+    """The reference's fine sample set (nerf.py:284-295: sort(cat(z_coarse, sample_fine,
+    sample_fine_depth))) recomputed on the CPU from GIVEN coarse-pass outputs -- the HIP
+    ones, to check that a flipped ray's HIP samples are exactly what the reference
+    algorithm draws from the HIP coarse weights.  streams = (u_coarse, u_fine, u_fine_jit,
+    n_depth); returns (B, Kc + Kf)."""
+    from . import ref_cpu
+
+    rays = rays.reshape(-1, 8).float().cpu()
+    B = rays.shape[0]
+    parts = [z_coarse.reshape(B, -1).float().cpu()]
+    nf = n_fine - n_fine_depth
+    if nf > 0:
+        parts.append(ref_cpu.sample_fine(rays, w_coarse.reshape(B, -1).float().cpu(), n_coarse,
+                                         streams[1].reshape(B, -1), streams[2].reshape(B, -1), lindisp))
+    if n_fine_depth > 0:
+        parts.append(ref_cpu.sample_fine_depth(rays, depth_coarse.reshape(B).float().cpu(), n_fine_depth,
+                                               depth_std, streams[3].reshape(B, -1)))
+    return torch.sort(torch.cat(parts, -1), -1)[0]
+
+
+def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref, z_expected_hip=None):
     """Classify the fine pass of B rays.
 
     Returns a dict of (B,) bool masks:
@@ -64,6 +86,9 @@ def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref):
                     cdf scan and torch's fp32 cumsum round a boundary differently);
       z_differs   — the returned sorted fine samples differ beyond the fp32 tolerance;
       unexplained — z_differs but no bin differs (must be empty: a kernel bug);
+      inconsistent — (with ``z_expected_hip``, from ``expected_fine_z`` on the HIP coarse
+                    outputs) a flipped ray whose HIP samples are NOT the reference
+                    algorithm's draw from the HIP coarse weights (must be empty);
     plus ``flip_idx`` (list of ray indices) for messages."""
     B = z_fine_ref.shape[0]
     zh = z_fine_hip.detach().float().cpu().reshape(B, -1)
@@ -79,5 +104,9 @@ def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref):
     z_differs = ~close_mask(zh, zr).all(-1)
     flip = bins_differ | (marginal & z_differs)
     unexplained = z_differs & ~flip
-    return dict(flip=flip, z_differs=z_differs, unexplained=unexplained,
+    inconsistent = torch.zeros(B, dtype=torch.bool)
+    if z_expected_hip is not None:
+        ze = z_expected_hip.detach().float().cpu().reshape(B, -1)
+        inconsistent = flip & ~close_mask(zh, ze).all(-1)
+    return dict(flip=flip, z_differs=z_differs, unexplained=unexplained, inconsistent=inconsistent,
                 flip_idx=[int(i) for i in torch.nonzero(flip).reshape(-1)])

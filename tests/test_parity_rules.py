@@ -1,0 +1,60 @@
+"""The fine-pass flip rule of the parity tests (oracle/parity.py), on CPU.
+
+A searchsorted bin flip is proven from the coarse weights: these tests perturb the
+reference's coarse weights of a fixture (as the HIP reduction order does, but larger),
+redraw the fine samples from the perturbed weights with the reference algorithm, and check
+that the classifier flags exactly the rays whose bins moved, and catches both kinds of
+kernel bug: a fine sample set that differs without a flip, and a flipped ray whose samples
+do not follow its own coarse weights.
+"""
+import torch
+
+import fixtures
+from oracle import parity
+
+
+def _case(scale):
+    cfg, arr = fixtures.load("fw_cfg2_b128")
+    B = arr["rays"].reshape(-1, 8).shape[0]
+    w_ref = arr["coarse_weights"].reshape(B, -1)
+    g = torch.Generator().manual_seed(3)
+    w_hip = w_ref * (1.0 + scale * torch.randn(w_ref.shape, generator=g))
+    streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
+    z_hip = parity.expected_fine_z(arr["rays"], arr["z_coarse"], w_hip, arr["coarse_depth"], streams,
+                                   cfg["n_coarse"], cfg["n_fine"], cfg["n_fine_depth"])
+    return cfg, arr, B, w_ref, w_hip, z_hip
+
+
+def test_expected_fine_z_reproduces_the_reference_samples():
+    cfg, arr, B, w_ref, _, _ = _case(0.0)
+    streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
+    z = parity.expected_fine_z(arr["rays"], arr["z_coarse"], w_ref, arr["coarse_depth"], streams,
+                               cfg["n_coarse"], cfg["n_fine"], cfg["n_fine_depth"])
+    torch.testing.assert_close(z, arr["z_fine"].reshape(B, -1), atol=1e-6, rtol=0)
+
+
+def test_flips_are_exactly_the_rays_whose_bins_moved():
+    cfg, arr, B, w_ref, w_hip, z_hip = _case(2e-3)
+    bins_moved = (parity.fine_bins(w_hip, arr["u_fine"]) != parity.fine_bins(w_ref, arr["u_fine"])).any(-1)
+    assert 0 < int(bins_moved.sum()) < B
+    cls = parity.classify_fine(w_hip, w_ref, arr["u_fine"], z_hip, arr["z_fine"], z_hip)
+    assert torch.equal(cls["flip"], bins_moved)
+    assert not cls["unexplained"].any() and not cls["inconsistent"].any()
+    # every ray without a flip has the reference's samples
+    keep = ~cls["flip"]
+    torch.testing.assert_close(z_hip[keep], arr["z_fine"].reshape(B, -1)[keep], atol=1e-6, rtol=0)
+
+
+def test_classifier_catches_sample_errors():
+    cfg, arr, B, w_ref, w_hip, z_hip = _case(2e-3)
+    cls = parity.classify_fine(w_hip, w_ref, arr["u_fine"], z_hip, arr["z_fine"], z_hip)
+    ok_ray = int(torch.nonzero(~cls["flip"])[0])
+    flip_ray = int(torch.nonzero(cls["flip"])[0])
+    bad = z_hip.clone()
+    bad[ok_ray, 5] += 1e-3          # a sample moved on a ray whose bins did not
+    cls = parity.classify_fine(w_hip, w_ref, arr["u_fine"], bad, arr["z_fine"], z_hip)
+    assert cls["unexplained"].nonzero().reshape(-1).tolist() == [ok_ray]
+    bad = z_hip.clone()
+    bad[flip_ray, 7] += 1e-3        # a flipped ray that does not follow its own weights
+    cls = parity.classify_fine(w_hip, w_ref, arr["u_fine"], bad, arr["z_fine"], z_hip)
+    assert cls["inconsistent"].nonzero().reshape(-1).tolist() == [flip_ray]
