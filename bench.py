@@ -615,7 +615,7 @@ def psnr_vs_reference_path(net, rays_dev, ref, streams, dev):
     with torch.no_grad():
         out = r(net, rays_dev[None].contiguous(), want_weights=True)
     tgt = torch.from_numpy(synth.hash_uniform(5, n * 3).astype("float32")).reshape(n, 3)
-    z_exp = parity.expected_fine_z(rays_dev, out.coarse.z, out.coarse.weights, out.coarse.depth, streams,
+    z_exp = parity.expected_fine_sets(rays_dev, out.coarse.z, out.coarse.weights, out.coarse.depth, streams,
                                    KC, KF, 0)
     cls = parity.classify_fine(out.coarse.weights[0], ref["coarse"]["weights"][0], streams[1],
                                out.fine.z[0], ref["fine"]["z"], z_exp)

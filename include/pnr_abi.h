@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 1
+#define PNR_ABI_VERSION 2
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -102,12 +102,28 @@ typedef struct pnr_rays {
     int64_t rays_per_obj;
 } pnr_rays;
 
-/* Random streams, drawn in the reference's order (nerf.py:111, 135, 141, 158). */
+/* Random draws of the march (nerf.py:111, 135, 141, 158), in one of two modes:
+ *   injected  the four streams below, drawn by the caller in the reference's order (tests
+ *             and fixtures: the reference's own torch.rand draws replayed exactly);
+ *   counter   every stream pointer NULL: the kernels draw on device from {seed, offset}
+ *             with Philox4x32-10.  Draw k of ray b of stream s uses the counter
+ *             (lo32 e, hi32 e, s, 0), e = (offset + b) * width_s + k, key (lo32 seed,
+ *             hi32 seed); U[0,1) = (word0 >> 8) * 2^-24; N(0,1) = Box-Muller on
+ *             u1 = ((word0 >> 8) + 1) * 2^-24, u2 = (word1 >> 8) * 2^-24.  A ray's draws
+ *             depend on its global index (offset + b) only, so chunking a batch with
+ *             offset = the chunk's first ray gives the same samples as one call.
+ *             No HBM streams are written or read.  pnr_rng_fill materialises a stream. */
+#define PNR_RNG_U_COARSE 0   /* width n_coarse                      */
+#define PNR_RNG_U_FINE 1     /* width n_fine - n_fine_depth         */
+#define PNR_RNG_U_FINE_JIT 2 /* width n_fine - n_fine_depth         */
+#define PNR_RNG_N_DEPTH 3    /* width n_fine_depth, normal          */
 typedef struct pnr_rng {
     const float *u_coarse;   /* (n_rays, n_coarse)          U[0,1)  */
     const float *u_fine;     /* (n_rays, n_fine - n_fine_depth)     */
     const float *u_fine_jit; /* (n_rays, n_fine - n_fine_depth)     */
     const float *n_depth;    /* (n_rays, n_fine_depth)      N(0,1)  */
+    uint64_t seed;           /* counter mode (all four pointers NULL) */
+    uint64_t offset;         /* global index of ray 0 of this call    */
 } pnr_rng;
 
 typedef struct pnr_render_cfg {
@@ -234,6 +250,14 @@ int pnr_sample_fine(const float *rays, int64_t n_rays, int32_t n_coarse,
 int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n_rays,
                   int32_t k, int32_t white_bkgd, float *weights, float *rgb, float *depth,
                   pnr_stream_t stream);
+
+/* ---- counter-mode draws --------------------------------------------------------- */
+/* Replaces: the torch.rand / torch.randn draws of the march (nerf.py:111, 135, 141, 158) in
+ * counter mode: writes out (n_rays, width) = the draws of `stream` (PNR_RNG_*) for rays
+ * offset .. offset + n_rays - 1 exactly as the render kernels draw them (uniform for
+ * streams 0-2, normal for 3). */
+int pnr_rng_fill(uint64_t seed, uint64_t offset, int32_t stream, int64_t n_rays, int32_t width, float *out,
+                 pnr_stream_t stream_h);
 
 /* ---- ray generation ------------------------------------------------------------ */
 /* Replaces: util.gen_rays (util.py:238-276) with unproj_map (util.py:113-143), ndc=False.

@@ -54,13 +54,36 @@ def close_mask(a, b, atol=ATOL, rtol=RTOL):
     return (a - b).abs() <= atol + rtol * b.abs()
 
 
+def _marginal_alt_fine(rays, w_coarse, n_coarse, u, u_jit, lindisp):
+    """sample_fine (nerf.py:126-148) with every draw that sits within MARGIN of a boundary
+    of the cdf built from ``w_coarse`` moved to the bin on the OTHER side of that boundary.
+    The device sums the pdf normaliser and scans the cdf in a different order than torch,
+    so a draw placed on a boundary (the fixtures' force_u_high rays, u = 1 - 2^-24 against
+    cdf[-1] = 1 +- ulp) may land in either neighbouring bin from the same weights."""
+    cdf = fine_cdf(w_coarse)
+    u = u.float().cpu().reshape(cdf.shape[0], -1)
+    ind = torch.clamp_min(torch.searchsorted(cdf, u.contiguous(), right=True) - 1, 0)
+    dist = (u.unsqueeze(-1) - cdf.unsqueeze(1)).abs()
+    near_j = dist.argmin(-1)                             # nearest boundary cdf[j]
+    marginal = dist.amin(-1) <= MARGIN
+    # u >= cdf[j] gives bin j; u < cdf[j] gives bin j - 1: take the other one
+    alt = torch.where(ind >= near_j, near_j - 1, near_j).clamp_min(0)
+    ind = torch.where(marginal, alt, ind).float()
+    z_steps = (ind + u_jit.float().cpu().reshape(u.shape)) / n_coarse
+    near, far = rays[:, -2:-1], rays[:, -1:]
+    if not lindisp:
+        return near * (1 - z_steps) + far * z_steps
+    return 1 / (1 / near * (1 - z_steps) + 1 / far * z_steps)
+
+
 def expected_fine_z(rays, z_coarse, w_coarse, depth_coarse, streams, n_coarse, n_fine, n_fine_depth,
-                    depth_std=0.01, lindisp=False):
+                    depth_std=0.01, lindisp=False, marginal_alt=False):
     """The reference's fine sample set (nerf.py:284-295: sort(cat(z_coarse, sample_fine,
     sample_fine_depth))) recomputed on the CPU from GIVEN coarse-pass outputs -- the HIP
     ones, to check that a flipped ray's HIP samples are exactly what the reference
     algorithm draws from the HIP coarse weights.  streams = (u_coarse, u_fine, u_fine_jit,
-    n_depth); returns (B, Kc + Kf)."""
+    n_depth); returns (B, Kc + Kf).  ``marginal_alt``: draws within MARGIN of a cdf
+    boundary take the other neighbouring bin (``_marginal_alt_fine``)."""
     from . import ref_cpu
 
     rays = rays.reshape(-1, 8).float().cpu()
@@ -68,12 +91,20 @@ def expected_fine_z(rays, z_coarse, w_coarse, depth_coarse, streams, n_coarse, n
     parts = [z_coarse.reshape(B, -1).float().cpu()]
     nf = n_fine - n_fine_depth
     if nf > 0:
-        parts.append(ref_cpu.sample_fine(rays, w_coarse.reshape(B, -1).float().cpu(), n_coarse,
-                                         streams[1].reshape(B, -1), streams[2].reshape(B, -1), lindisp))
+        w = w_coarse.reshape(B, -1).float().cpu()
+        u, uj = streams[1].reshape(B, -1), streams[2].reshape(B, -1)
+        parts.append(_marginal_alt_fine(rays, w, n_coarse, u, uj, lindisp) if marginal_alt
+                     else ref_cpu.sample_fine(rays, w, n_coarse, u, uj, lindisp))
     if n_fine_depth > 0:
         parts.append(ref_cpu.sample_fine_depth(rays, depth_coarse.reshape(B).float().cpu(), n_fine_depth,
                                                depth_std, streams[3].reshape(B, -1)))
     return torch.sort(torch.cat(parts, -1), -1)[0]
+
+
+def expected_fine_sets(*args, **kw):
+    """(expected_fine_z(...), expected_fine_z(..., marginal_alt=True)): the two sample sets a
+    flipped ray may take from its own coarse weights (pass to ``classify_fine``)."""
+    return expected_fine_z(*args, **kw), expected_fine_z(*args, marginal_alt=True, **kw)
 
 
 def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref, z_expected_hip=None):
@@ -87,8 +118,9 @@ def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref, z_
       z_differs   — the returned sorted fine samples differ beyond the fp32 tolerance;
       unexplained — z_differs but no bin differs (must be empty: a kernel bug);
       inconsistent — (with ``z_expected_hip``, from ``expected_fine_z`` on the HIP coarse
-                    outputs) a flipped ray whose HIP samples are NOT the reference
-                    algorithm's draw from the HIP coarse weights (must be empty);
+                    outputs, or a tuple of it and its ``marginal_alt=True`` variant) a
+                    flipped ray whose HIP samples are NOT the reference algorithm's draw
+                    from the HIP coarse weights (must be empty);
     plus ``flip_idx`` (list of ray indices) for messages."""
     B = z_fine_ref.shape[0]
     zh = z_fine_hip.detach().float().cpu().reshape(B, -1)
@@ -106,7 +138,11 @@ def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref, z_
     unexplained = z_differs & ~flip
     inconsistent = torch.zeros(B, dtype=torch.bool)
     if z_expected_hip is not None:
-        ze = z_expected_hip.detach().float().cpu().reshape(B, -1)
-        inconsistent = flip & ~close_mask(zh, ze).all(-1)
+        # a tuple: the expected set and its marginal-draw alternative (either may match)
+        sets = z_expected_hip if isinstance(z_expected_hip, (tuple, list)) else (z_expected_hip,)
+        follows = torch.zeros(B, dtype=torch.bool)
+        for ze in sets:
+            follows |= close_mask(zh, ze.detach().float().cpu().reshape(B, -1)).all(-1)
+        inconsistent = flip & ~follows
     return dict(flip=flip, z_differs=z_differs, unexplained=unexplained, inconsistent=inconsistent,
                 flip_idx=[int(i) for i in torch.nonzero(flip).reshape(-1)])

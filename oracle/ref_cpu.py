@@ -225,27 +225,35 @@ def _points(rays, z):
 
 
 def render(model_fn, rays, n_coarse, n_fine, n_fine_depth, streams, white_bkgd,
-           lindisp=False, depth_std=0.01):
+           lindisp=False, depth_std=0.01, using_fine=None, sigma_noise=None):
     """nerf.py:251-303.  ``model_fn(points (SB, P, 3), coarse, viewdirs) -> (SB, P, 4)``;
-    ``streams`` = (u_coarse, u_fine, u_fine_jit, n_depth).  Returns a dict
+    ``streams`` = (u_coarse, u_fine, u_fine_jit, n_depth).  ``using_fine`` (default
+    n_fine > 0) is the flag nerf.py:87 fixes at construction: with it set and no fine
+    samples, the fine pass re-evaluates the coarse samples (nerf.py:284-298).
+    ``sigma_noise`` = (coarse (B, Kc), fine (B, K)) N(0,1)·noise_std draws added to sigma
+    before compositing (training mode, nerf.py:225-226).  Returns a dict
     {"coarse": {rgb, depth, weights, z}, "fine": {...}} shaped (SB, B', ...)."""
     u_c, u_f, u_j, n_d = streams
     SB = rays.shape[0]
     rays = rays.reshape(-1, 8)
     B = rays.shape[0]
+    if using_fine is None:
+        using_fine = n_fine > 0
 
     def one_pass(z, coarse):
         pts, dirs = _points(rays, z)
         K = z.shape[1]
-        raw = model_fn(pts.reshape(SB, -1, 3), coarse, dirs.reshape(SB, -1, 3))
-        w, rgb, depth = composite(rays, z, raw.reshape(B, K, -1), white_bkgd)
+        raw = model_fn(pts.reshape(SB, -1, 3), coarse, dirs.reshape(SB, -1, 3)).reshape(B, K, -1)
+        if sigma_noise is not None:
+            raw = torch.cat([raw[..., :3], raw[..., 3:] + sigma_noise[0 if coarse else 1].unsqueeze(-1)], -1)
+        w, rgb, depth = composite(rays, z, raw, white_bkgd)
         return dict(rgb=rgb.reshape(SB, -1, 3), depth=depth.reshape(SB, -1),
                     weights=w.reshape(SB, -1, K), z=z, raw=raw.reshape(-1, 4),
                     _w=w, _depth=depth)
 
     z_c = sample_coarse(rays, n_coarse, u_c, lindisp)
     out = {"coarse": one_pass(z_c, True)}
-    if n_fine > 0:
+    if using_fine:
         samps = [z_c]
         if n_fine - n_fine_depth > 0:
             samps.append(sample_fine(rays, out["coarse"]["_w"], n_coarse, u_f, u_j, lindisp))

@@ -11,10 +11,11 @@
 namespace pnr {
 
 // launchers (march.hip, mlp.hip)
-int launch_sample_coarse(const float *, int64_t, int, const float *, int, float *, hipStream_t);
+int launch_sample_coarse(const float *, int64_t, int, const RngSrc &, int, float *, hipStream_t);
 int launch_sample_fine(const float *, int64_t, int, const float *, const float *, const float *,
-                       int, int, float, const float *, const float *, const float *, int, float *,
+                       int, int, float, const RngSrc &, const RngSrc &, const RngSrc &, int, float *,
                        hipStream_t, int *origin = nullptr, float *z_new = nullptr);
+int launch_rng_fill(const RngSrc &, int64_t, int, float *, hipStream_t);
 int launch_merge_raw(const int *, const float *, const float *, int64_t, int, int, float *, hipStream_t);
 int launch_gen_rays(const float *, int64_t, int, int, int, float, float, float, float, float, float,
                     float *, hipStream_t);
@@ -344,9 +345,17 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     if (rays->rays_per_obj <= 0 || n % rays->rays_per_obj != 0 || n / rays->rays_per_obj != scene->n_obj)
         return fail(PNR_ERR_INVALID, "n_rays (%lld) must be n_obj (%d) x rays_per_obj (%lld)",
                     (long long)n, scene->n_obj, (long long)rays->rays_per_obj);
-    if (!rng->u_coarse) return fail(PNR_ERR_INVALID, "u_coarse stream is NULL");
-    if (kf - kfd > 0 && (!rng->u_fine || !rng->u_fine_jit)) return fail(PNR_ERR_INVALID, "fine streams NULL");
-    if (kfd > 0 && !rng->n_depth) return fail(PNR_ERR_INVALID, "n_depth stream NULL");
+    // injected streams, or counter mode when every stream pointer is NULL (pnr_abi.h)
+    const bool counter = !rng->u_coarse && !rng->u_fine && !rng->u_fine_jit && !rng->n_depth;
+    if (!counter) {
+        if (!rng->u_coarse) return fail(PNR_ERR_INVALID, "u_coarse stream is NULL");
+        if (kf - kfd > 0 && (!rng->u_fine || !rng->u_fine_jit)) return fail(PNR_ERR_INVALID, "fine streams NULL");
+        if (kfd > 0 && !rng->n_depth) return fail(PNR_ERR_INVALID, "n_depth stream NULL");
+    }
+    const RngSrc r_uc{rng->u_coarse, rng->seed, rng->offset, PNR_RNG_U_COARSE};
+    const RngSrc r_uf{rng->u_fine, rng->seed, rng->offset, PNR_RNG_U_FINE};
+    const RngSrc r_uj{rng->u_fine_jit, rng->seed, rng->offset, PNR_RNG_U_FINE_JIT};
+    const RngSrc r_nd{rng->n_depth, rng->seed, rng->offset, PNR_RNG_N_DEPTH};
     if (!out->coarse_rgb || !out->coarse_depth) return fail(PNR_ERR_INVALID, "coarse outputs NULL");
     if (kf > 0 && (!out->fine_rgb || !out->fine_depth)) return fail(PNR_ERR_INVALID, "fine outputs NULL");
     const RenderWs w = render_ws(scene, cfg, n);
@@ -366,7 +375,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
 
     // coarse pass (nerf.py:273-276)
     if ((rc = mark(0))) return rc;
-    if ((rc = launch_sample_coarse(rays->rays, n, kc, rng->u_coarse, cfg->lindisp, zc, st))) return rc;
+    if ((rc = launch_sample_coarse(rays->rays, n, kc, r_uc, cfg->lindisp, zc, st))) return rc;
     if ((rc = mark(1))) return rc;
     if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj,
                                nullptr, nullptr, 1, n * kc, rawc, xsum, st, nullptr, coarse_proj)))
@@ -388,7 +397,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     int *origin = reuse ? reinterpret_cast<int *>(ws + w.origin) : nullptr;
     float *z_new = reuse ? reinterpret_cast<float *>(ws + w.z_new) : nullptr;
     if ((rc = launch_sample_fine(rays->rays, n, kc, zc, wc, out->coarse_depth, kf, kfd, cfg->depth_std,
-                                 rng->u_fine, rng->u_fine_jit, rng->n_depth, cfg->lindisp, zf, st, origin, z_new)))
+                                 r_uf, r_uj, r_nd, cfg->lindisp, zf, st, origin, z_new)))
         return rc;
     if ((rc = mark(4))) return rc;
     if (reuse) {
@@ -412,7 +421,8 @@ int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse, const
                       int32_t lindisp, float *z, pnr_stream_t stream) {
     if (n_rays < 0 || n_coarse < 1) return fail(PNR_ERR_INVALID, "pnr_sample_coarse: bad sizes");
     if (n_rays > 0 && (!rays || !u_coarse || !z)) return fail(PNR_ERR_INVALID, "pnr_sample_coarse: NULL");
-    return launch_sample_coarse(rays, n_rays, n_coarse, u_coarse, lindisp, z, (hipStream_t)stream);
+    return launch_sample_coarse(rays, n_rays, n_coarse, RngSrc{u_coarse, 0, 0, PNR_RNG_U_COARSE}, lindisp, z,
+                                (hipStream_t)stream);
 }
 
 int pnr_sample_fine(const float *rays, int64_t n_rays, int32_t n_coarse, const float *z_coarse,
@@ -428,8 +438,18 @@ int pnr_sample_fine(const float *rays, int64_t n_rays, int32_t n_coarse, const f
     if (n_fine - n_fine_depth > 0 && (!u_fine || !u_fine_jit)) return fail(PNR_ERR_INVALID, "fine streams NULL");
     if (n_fine_depth > 0 && (!n_depth || !coarse_depth)) return fail(PNR_ERR_INVALID, "depth inputs NULL");
     return launch_sample_fine(rays, n_rays, n_coarse, z_coarse, coarse_weights, coarse_depth, n_fine,
-                              n_fine_depth, depth_std, u_fine, u_fine_jit, n_depth, lindisp, z_fine,
-                              (hipStream_t)stream);
+                              n_fine_depth, depth_std, RngSrc{u_fine, 0, 0, PNR_RNG_U_FINE},
+                              RngSrc{u_fine_jit, 0, 0, PNR_RNG_U_FINE_JIT}, RngSrc{n_depth, 0, 0, PNR_RNG_N_DEPTH},
+                              lindisp, z_fine, (hipStream_t)stream);
+}
+
+int pnr_rng_fill(uint64_t seed, uint64_t offset, int32_t stream, int64_t n_rays, int32_t width, float *out,
+                 pnr_stream_t stream_h) {
+    if (stream < PNR_RNG_U_COARSE || stream > PNR_RNG_N_DEPTH) return fail(PNR_ERR_INVALID, "pnr_rng_fill: bad stream");
+    if (n_rays < 0 || width < 0) return fail(PNR_ERR_INVALID, "pnr_rng_fill: bad sizes");
+    if (n_rays * (int64_t)width == 0) return PNR_OK;
+    if (!out) return fail(PNR_ERR_INVALID, "pnr_rng_fill: NULL");
+    return launch_rng_fill(RngSrc{nullptr, seed, offset, stream}, n_rays, width, out, (hipStream_t)stream_h);
 }
 
 int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n_rays, int32_t k,

@@ -22,8 +22,7 @@ __device__ __forceinline__ float linspace_at(int i, int n, float end, float step
 }
 
 __global__ void k_sample_coarse(const float *__restrict__ rays, int64_t n_rays, int kc,
-                                const float *__restrict__ u, int lindisp,
-                                float *__restrict__ z) {
+                                const RngSrc u, int lindisp, float *__restrict__ z) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n_rays * kc) return;
     const int64_t b = idx / kc;
@@ -32,7 +31,7 @@ __global__ void k_sample_coarse(const float *__restrict__ rays, int64_t n_rays, 
     const float end = (float)(1.0 - 1.0 / (double)kc);
     const float lstep = (kc > 1) ? __fdiv_rn(end, (float)(kc - 1)) : 0.0f;
     const float step = (float)(1.0 / (double)kc);
-    float t = add_rn(linspace_at(k, kc, end, lstep), mul_rn(u[idx], step));
+    float t = add_rn(linspace_at(k, kc, end, lstep), mul_rn(rng_uniform(u, b, kc, k), step));
     z[idx] = t_to_z(t, near, far, lindisp != 0);
 }
 
@@ -43,8 +42,8 @@ __global__ void k_sample_coarse(const float *__restrict__ rays, int64_t n_rays, 
 __global__ __launch_bounds__(64) void k_sample_fine(
     const float *__restrict__ rays, int kc, const float *__restrict__ z_coarse,
     const float *__restrict__ weights, const float *__restrict__ depth, int kf, int kfd,
-    float depth_std, const float *__restrict__ u_fine, const float *__restrict__ u_jit,
-    const float *__restrict__ n_depth, int lindisp, int n_sort, float *__restrict__ z_fine,
+    float depth_std, const RngSrc u_fine, const RngSrc u_jit, const RngSrc n_depth, int lindisp,
+    int n_sort, float *__restrict__ z_fine,
     int *__restrict__ origin, float *__restrict__ z_new) {
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *cdf = smem;            // kc + 1
@@ -80,7 +79,7 @@ __global__ __launch_bounds__(64) void k_sample_fine(
     const float inv_steps = (float)kc;
     // importance samples (nerf.py:135-148)
     for (int j = lane; j < nf; j += 64) {
-        const float u = u_fine[b * nf + j];
+        const float u = rng_uniform(u_fine, b, nf, j);
         // searchsorted(cdf, u, right=True): number of cdf entries <= u
         int lo = 0, hi = kc + 1;
         while (lo < hi) {
@@ -88,12 +87,12 @@ __global__ __launch_bounds__(64) void k_sample_fine(
             if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
         }
         float ind = fmaxf(sub_rn((float)lo, 1.0f), 0.0f);
-        float t = __fdiv_rn(add_rn(ind, u_jit[b * nf + j]), inv_steps);
+        float t = __fdiv_rn(add_rn(ind, rng_uniform(u_jit, b, nf, j)), inv_steps);
         s[kc + j] = t_to_z(t, near, far, lindisp != 0);
     }
     // depth samples (nerf.py:157-160): clamp(depth + N(0,1) * std, near, far)
     for (int j = lane; j < kfd; j += 64) {
-        float zz = add_rn(depth[b], mul_rn(n_depth[b * kfd + j], depth_std));
+        float zz = add_rn(depth[b], mul_rn(rng_normal(n_depth, b, kfd, j), depth_std));
         s[kc + nf + j] = fmaxf(fminf(zz, far), near);
     }
     for (int k = lane; k < kc; k += 64) s[k] = z_coarse[b * kc + k];
@@ -327,7 +326,7 @@ __global__ __launch_bounds__(256) void k_gen_rays(const float *__restrict__ pose
 // ---------------------------------------------------------------------------
 // host launchers (validated by the extern "C" layer in abi.cpp)
 // ---------------------------------------------------------------------------
-int launch_sample_coarse(const float *rays, int64_t n_rays, int kc, const float *u, int lindisp,
+int launch_sample_coarse(const float *rays, int64_t n_rays, int kc, const RngSrc &u, int lindisp,
                          float *z, hipStream_t st) {
     const int64_t n = n_rays * kc;
     if (n == 0) return PNR_OK;
@@ -345,8 +344,8 @@ int sort_width(int n) {
 
 int launch_sample_fine(const float *rays, int64_t n_rays, int kc, const float *z_coarse,
                        const float *weights, const float *depth, int kf, int kfd,
-                       float depth_std, const float *u_fine, const float *u_jit,
-                       const float *n_depth, int lindisp, float *z_fine, hipStream_t st,
+                       float depth_std, const RngSrc &u_fine, const RngSrc &u_jit,
+                       const RngSrc &n_depth, int lindisp, float *z_fine, hipStream_t st,
                        int *origin, float *z_new) {
     if (n_rays == 0) return PNR_OK;
     const int n_sort = sort_width(kc + kf);
@@ -387,6 +386,25 @@ int launch_gen_rays(const float *poses, int64_t n_images, int pose_rows, int wid
     hipLaunchKernelGGL(k_gen_rays, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, poses, pose_rows,
                        n, width, height, fx, fy, cx, cy, near, far, rays);
     return launch_ok("gen_rays") ? PNR_OK : PNR_ERR_HIP;
+}
+
+// ---------------------------------------------------------------------------
+// counter-mode draws materialised (pnr_rng_fill): the same rng_uniform / rng_normal the
+// samplers call, one thread per draw
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rng_fill(const RngSrc r, int64_t n_rays, int width, float *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_rays * width) return;
+    const int64_t b = i / width;
+    const int k = (int)(i - b * width);
+    out[i] = r.stream == PNR_RNG_N_DEPTH ? rng_normal(r, b, width, k) : rng_uniform(r, b, width, k);
+}
+
+int launch_rng_fill(const RngSrc &r, int64_t n_rays, int width, float *out, hipStream_t st) {
+    const int64_t n = n_rays * width;
+    if (n == 0) return PNR_OK;
+    hipLaunchKernelGGL(k_rng_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, r, n_rays, width, out);
+    return launch_ok("rng_fill") ? PNR_OK : PNR_ERR_HIP;
 }
 
 }  // namespace pnr

@@ -92,6 +92,62 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// ---- counter-based random streams (pnr_rng {seed, offset}, include/pnr_abi.h) ----------
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1, 2, 3",
+// SC'11; the Random123 constants).  Draw e of stream s keyed by `seed` uses the counter
+// (lo32 e, hi32 e, s, 0); e = (offset + ray) * width + k, so a ray's draws depend only on
+// its global index and not on how the batch is chunked.  oracle/philox.py restates it.
+struct RngSrc {
+    const float *p;          // injected stream (n_rays, width); NULL = Philox
+    uint64_t seed, offset;
+    int stream;              // PNR_RNG_U_COARSE .. PNR_RNG_N_DEPTH
+};
+
+__device__ __forceinline__ void philox4x32_10(uint32_t &c0, uint32_t &c1, uint32_t &c2, uint32_t &c3,
+                                              uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        if (r) {
+            k0 += 0x9E3779B9u;
+            k1 += 0xBB67AE85u;
+        }
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0;
+        c1 = lo1;
+        c2 = n2;
+        c3 = lo0;
+    }
+}
+
+__device__ __forceinline__ void rng_bits(const RngSrc &r, int64_t ray, int width, int k, uint32_t &x0,
+                                         uint32_t &x1) {
+    const uint64_t e = (r.offset + (uint64_t)ray) * (uint64_t)width + (uint64_t)k;
+    uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(e >> 32), c2 = (uint32_t)r.stream, c3 = 0u;
+    philox4x32_10(c0, c1, c2, c3, (uint32_t)r.seed, (uint32_t)(r.seed >> 32));
+    x0 = c0;
+    x1 = c1;
+}
+
+// U[0, 1): the top 24 bits of the first Philox word times 2^-24 (exact in fp32)
+__device__ __forceinline__ float rng_uniform(const RngSrc &r, int64_t ray, int width, int k) {
+    if (r.p) return r.p[ray * width + k];
+    uint32_t x0, x1;
+    rng_bits(r, ray, width, k, x0, x1);
+    return (float)(x0 >> 8) * 0x1p-24f;
+}
+
+// N(0, 1) by Box-Muller on the first two words: u1 in (0, 1], u2 in [0, 1)
+__device__ __forceinline__ float rng_normal(const RngSrc &r, int64_t ray, int width, int k) {
+    if (r.p) return r.p[ray * width + k];
+    uint32_t x0, x1;
+    rng_bits(r, ray, width, k, x0, x1);
+    const float u1 = (float)((x0 >> 8) + 1u) * 0x1p-24f;
+    const float u2 = (float)(x1 >> 8) * 0x1p-24f;
+    return sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647f * u2);
+}
+
 // ---- exact 3-way bf16 split (split-bf16 products: mlp.hip PREC 6 / 9, wgrad.hip) ------
 typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));

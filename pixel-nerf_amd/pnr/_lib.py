@@ -47,7 +47,14 @@ class Rays(ctypes.Structure):
 
 
 class Rng(ctypes.Structure):
-    _fields_ = [("u_coarse", c_vp), ("u_fine", c_vp), ("u_fine_jit", c_vp), ("n_depth", c_vp)]
+    """Injected streams, or counter mode (Philox {seed, offset}) when all four are NULL."""
+    _fields_ = [("u_coarse", c_vp), ("u_fine", c_vp), ("u_fine_jit", c_vp), ("n_depth", c_vp),
+                ("seed", ctypes.c_uint64), ("offset", ctypes.c_uint64)]
+
+
+# pnr_rng counter-mode stream ids (PNR_RNG_*)
+RNG_U_COARSE, RNG_U_FINE, RNG_U_FINE_JIT, RNG_N_DEPTH = 0, 1, 2, 3
+ABI_VERSION = 2
 
 
 class RenderCfg(ctypes.Structure):
@@ -91,6 +98,7 @@ SIGNATURES = {
     "pnr_sample_fine": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f, c_vp,
                                 c_vp, c_vp, c_i32, c_vp, c_vp]),
     "pnr_composite": (c_i32, [c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp, c_vp]),
+    "pnr_rng_fill": (c_i32, [ctypes.c_uint64, ctypes.c_uint64, c_i32, c_i64, c_i32, c_vp, c_vp]),
     "pnr_gen_rays": (c_i32, [c_vp, c_i64, c_i32, c_i32, c_i32, c_f, c_f, c_f, c_f, c_f, c_f, c_vp, c_vp]),
     "pnr_latent_channels_last": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32),
                                          ctypes.POINTER(c_i32), c_i32, c_i32, c_vp, c_i32, c_i32, c_vp]),
@@ -134,6 +142,9 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.pnr_abi_version() != ABI_VERSION:
+        raise PnrError("libpnr.so ABI version %d, this binding expects %d; rebuild it"
+                       % (lib.pnr_abi_version(), ABI_VERSION))
     _lib = lib
     return lib
 

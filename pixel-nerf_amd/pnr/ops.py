@@ -69,3 +69,23 @@ def composite(z, raw, rays, white_bkgd, want_weights=True):
                                  int(bool(white_bkgd)), _lib.ptr(w), _lib.ptr(rgb), _lib.ptr(depth),
                                  _lib.stream_of(z.device)), "pnr_composite")
     return w, rgb, depth
+
+
+def rng_fill(seed, offset, stream, n_rays, width, device="cuda"):
+    """The counter-mode draws of one stream (pnr_rng_fill; include/pnr_abi.h pnr_rng):
+    (n_rays, width) for rays offset .. offset + n_rays - 1, exactly as the render kernels
+    draw them in counter mode.  stream: _lib.RNG_U_COARSE .. RNG_N_DEPTH."""
+    out = torch.empty(n_rays, width, device=device, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(lib.pnr_rng_fill(int(seed), int(offset), int(stream), int(n_rays), int(width), _lib.ptr(out),
+                                _lib.stream_of(out.device)), "pnr_rng_fill")
+    return out
+
+
+def rng_render_streams(seed, offset, n_rays, n_coarse, n_fine, n_fine_depth, device="cuda"):
+    """(u_coarse, u_fine, u_fine_jit, n_depth) of a counter-mode render call, materialised."""
+    nf = max(n_fine - n_fine_depth, 0)
+    return (rng_fill(seed, offset, _lib.RNG_U_COARSE, n_rays, n_coarse, device),
+            rng_fill(seed, offset, _lib.RNG_U_FINE, n_rays, nf, device),
+            rng_fill(seed, offset, _lib.RNG_U_FINE_JIT, n_rays, nf, device),
+            rng_fill(seed, offset, _lib.RNG_N_DEPTH, n_rays, n_fine_depth, device))

@@ -7,9 +7,16 @@ runs as one stream-ordered sequence in libpnr.so (``pnr_render_forward``).  Any
 other model goes through the reference's plug point ``model(points, coarse,
 viewdirs)`` with sampling and compositing still on the HIP kernels.
 
-Random draws keep the reference's order and shapes on the rays' device
-(nerf.py:111, 135, 141, 158): with the same torch seed this renderer consumes
-the generator exactly as the reference does.
+Random draws (nerf.py:111, 135, 141, 158), ``rng_mode``:
+  "counter" (default on the fused path) -- the kernels draw on device from a
+            Philox4x32-10 {seed, offset} (include/pnr_abi.h pnr_rng); the seed comes
+            from torch's default CPU generator once per call, so torch.manual_seed
+            still makes renders reproducible, and no stream tensors touch HBM;
+  "torch"   -- torch.rand / torch.randn on the rays' device in the reference's order
+            and shapes: with the same torch seed the generator is consumed exactly as
+            the reference consumes it.
+``streams`` (tests / benchmarks) injects explicit draws for one call.  The
+model-callback and training paths always draw with torch in the reference's order.
 """
 import torch
 
@@ -78,17 +85,29 @@ class NeRFRenderer(torch.nn.Module):
         self.register_buffer("last_sched", torch.tensor(0, dtype=torch.long), persistent=True)
         # test / benchmark hook: explicit (u_coarse, u_fine, u_fine_jit, n_depth)
         self.streams = None
+        self.rng_mode = "counter"
+        self.last_seed = None
+        # fused path: rays per library call (bounds the raw / z workspace, ~3 KB per ray at
+        # 64 + 64 samples); counter-mode draws do not depend on the chunking
+        self.max_rays_per_call = 1 << 20
         # test / benchmark hook: add each pass's sample depths ``z`` (SB, B', K) to the
         # output dicts (fine-pass parity is classified on them, oracle/parity.py)
         self.return_z = False
 
     # ---- random streams (nerf.py:111, 135, 141, 158) ---------------------------------
+    def fine_counts(self):
+        """(importance samples, depth samples) of the fine pass (nerf.py:284-293); (0, 0)
+        with ``using_fine`` still means a fine pass, over the coarse samples only."""
+        if not self.using_fine:
+            return 0, 0
+        return max(self.n_fine - self.n_fine_depth, 0), max(self.n_fine_depth, 0)
+
     def draw_streams(self, n_rays, device):
         if self.streams is not None:
             s = tuple(t.to(device=device, dtype=torch.float32).contiguous() for t in self.streams)
             self.streams = None
             return s
-        nf = self.n_fine - self.n_fine_depth
+        nf, kfd = self.fine_counts()
         u_c = torch.rand(n_rays, self.n_coarse, device=device)
         empty = torch.zeros(n_rays, 0, device=device)
         u_f = u_j = n_d = empty
@@ -96,8 +115,8 @@ class NeRFRenderer(torch.nn.Module):
             if nf > 0:
                 u_f = torch.rand(n_rays, nf, device=device)
                 u_j = torch.rand(n_rays, nf, device=device)
-            if self.n_fine_depth > 0:
-                n_d = torch.randn(n_rays, self.n_fine_depth, device=device)
+            if kfd > 0:
+                n_d = torch.randn(n_rays, kfd, device=device)
         return u_c, u_f, u_j, n_d
 
     # ---- building blocks (HIP) -------------------------------------------------------
@@ -142,16 +161,19 @@ class NeRFRenderer(torch.nn.Module):
         sb = rays.shape[0]
         rays = rays.reshape(-1, 8).contiguous()
         B = rays.shape[0]
-        if self.using_fine and self.n_fine <= 0:
-            raise NotImplementedError("using_fine with n_fine = 0 (fine pass over coarse samples only)")
         from .models import PixelNeRFNet
 
-        if isinstance(model, PixelNeRFNet) and torch.is_grad_enabled() and model.needs_grad():
-            return self._forward_train(model, rays, sb, want_weights)
-        streams = self.draw_streams(B, rays.device)
         if isinstance(model, PixelNeRFNet):
-            return self._forward_fused(model, rays, sb, streams, want_weights)
-        return self._forward_callback(model, rays, sb, streams, want_weights)
+            # the sigma noise of training mode (nerf.py:225-226) is added between the model
+            # and the composite, which the fused march does not expose: the training
+            # graph's kernels run it, with or without autograd
+            noisy = self.training and self.noise_std > 0.0
+            if noisy or (torch.is_grad_enabled() and model.needs_grad()):
+                return self._forward_train(model, rays, sb, want_weights)
+            if self.streams is None and self.rng_mode == "counter":
+                return self._forward_fused(model, rays, sb, None, want_weights)
+            return self._forward_fused(model, rays, sb, self.draw_streams(B, rays.device), want_weights)
+        return self._forward_callback(model, rays, sb, self.draw_streams(B, rays.device), want_weights)
 
     def _forward_train(self, net, rays, sb, want_weights):
         """The reference's autograd graph (nerf.py:251-303) over the HIP kernels
@@ -168,8 +190,8 @@ class NeRFRenderer(torch.nn.Module):
         if rays.device.type != "cuda":
             raise ValueError("pnr: rays must be on the HIP device")
         kc = self.n_coarse
-        kf = self.n_fine if self.using_fine else 0
-        kfd = self.n_fine_depth if self.using_fine else 0
+        nf, kfd = self.fine_counts()
+        kf = nf + kfd
         noisy = self.training and self.noise_std > 0.0
         B, dev = rays.shape[0], rays.device
         lazy = noisy and self.streams is None   # draws interleave with the noise draws
@@ -192,8 +214,7 @@ class NeRFRenderer(torch.nn.Module):
         raw_c = add_noise(RenderPoints.apply(net, True, rays, z_c, lat, *p_c))
         w_c, rgb_c, d_c = Composite.apply(z_c, raw_c.contiguous(), rays, self.white_bkgd)
         outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, d_c, sb, want_weights, z_c))
-        if kf > 0:
-            nf = kf - kfd
+        if self.using_fine:
             if lazy:
                 empty = torch.zeros(B, 0, device=dev)
                 u_f = torch.rand(B, nf, device=dev) if nf > 0 else empty
@@ -222,22 +243,51 @@ class NeRFRenderer(torch.nn.Module):
         return d
 
     def _forward_fused(self, net, rays, sb, streams, want_weights):
+        """The whole march in libpnr.so (pnr_render_forward_proj).  ``streams`` None =
+        counter-mode draws.  With ``using_fine`` and no fine samples the fine pass runs the
+        fine MLP over the coarse samples (nerf.py:284-298 with all_samps = [z_coarse]): a
+        second coarse-only march with the fine model and the same draws."""
         net._require_hip()
         if rays.device.type != "cuda":
             raise ValueError("pnr: rays must be on the HIP device")
-        if self.training and self.noise_std > 0.0:
-            raise NotImplementedError("noise_std > 0 in training mode is not implemented")
+        B = rays.shape[0]
+        kc = self.n_coarse
+        nf, kfd = self.fine_counts()
+        kf = nf + kfd
+        seed = None
+        if streams is None:
+            seed = int(torch.randint(0, 2 ** 63 - 1, (1,), dtype=torch.int64).item())
+            self.last_seed = seed   # the counter-mode key of the last call (tests replay it)
+        # one object: ray chunks of max_rays_per_call (several objects: one call, the scene
+        # record covers them all)
+        step = max(1, int(self.max_rays_per_call)) if sb == 1 else max(B, 1)
+        parts = []
+        for r0 in range(0, max(B, 1), step):
+            r1 = min(B, r0 + step)
+            st = None if streams is None else tuple(t[r0:r1] for t in streams)
+            if self.using_fine and kf == 0:
+                out = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, 0, 0, True, want_weights)
+                fine = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, 0, 0, False, want_weights)
+                out.fine = fine.coarse
+            else:
+                out = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, kf, kfd, True, want_weights)
+            parts.append(out)
+        if len(parts) == 1:
+            return parts[0]
+        return DotMap({p: DotMap({k: torch.cat([o[p][k] for o in parts], 1) for k in parts[0][p]})
+                       for p in parts[0]})
+
+    def _fused_call(self, net, rays, sb, streams, seed, offset, kc, kf, kfd, coarse, want_weights):
+        """One pnr_render_forward_proj call.  coarse=False: the fine MLP in the coarse slot
+        (a coarse-only march with the fine model)."""
         B = rays.shape[0]
         dev = rays.device
-        kc, kf = self.n_coarse, (self.n_fine if self.using_fine else 0)
-        kfd = self.n_fine_depth if self.using_fine else 0
-        u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
         cfg = _lib.RenderCfg(kc, kf, kfd, float(self.depth_std), int(bool(self.white_bkgd)),
                              int(bool(self.lindisp)))
         sc = net.hip_scene()
-        desc, pc = net.hip_mlp(True)
+        desc, pc = net.hip_mlp(coarse)
         _, pf = net.hip_mlp(False) if kf > 0 else (None, None)
-        zc = net.hip_proj(True, sc)
+        zc = net.hip_proj(coarse, sc)
         zf = net.hip_proj(False, sc) if kf > 0 else None
         f32 = dict(device=dev, dtype=torch.float32)
         c_rgb, c_depth = torch.empty(B, 3, **f32), torch.empty(B, **f32)
@@ -255,9 +305,13 @@ class NeRFRenderer(torch.nn.Module):
                              z_c.data_ptr() if z_c is not None else None,
                              z_f.data_ptr() if z_f is not None else None)
         r = _lib.Rays(rays.data_ptr(), B, B // sb)
-        rng = _lib.Rng(u_c.data_ptr(), u_f.data_ptr() if u_f.numel() else None,
-                       u_j.data_ptr() if u_j.numel() else None,
-                       n_d.data_ptr() if n_d.numel() else None)
+        if streams is None:
+            rng = _lib.Rng(None, None, None, None, seed, offset)
+        else:
+            u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
+            rng = _lib.Rng(u_c.data_ptr(), u_f.data_ptr() if u_f.numel() else None,
+                           u_j.data_ptr() if u_j.numel() else None,
+                           n_d.data_ptr() if n_d.numel() else None, 0, 0)
         lib = _lib.load()
         ws_bytes = lib.pnr_render_workspace_bytes(sc, cfg, B)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
@@ -275,8 +329,9 @@ class NeRFRenderer(torch.nn.Module):
         w_c, rgb_c, depth_c = self.composite(model, rays, z_c, coarse=True, sb=sb)
         outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, depth_c, sb, want_weights, z_c))
         if self.using_fine:
-            z_f = ops.sample_fine(rays, z_c, w_c.detach(), depth_c, self.n_fine, self.n_fine_depth,
-                                  self.depth_std, u_f, u_j, n_d, self.lindisp)
+            nf, kfd = self.fine_counts()
+            z_f = z_c if nf + kfd == 0 else ops.sample_fine(rays, z_c, w_c.detach(), depth_c, nf + kfd, kfd,
+                                                            self.depth_std, u_f, u_j, n_d, self.lindisp)
             w_f, rgb_f, depth_f = self.composite(model, rays, z_f, coarse=False, sb=sb)
             outputs.fine = self._pack_out(w_f, rgb_f, depth_f, sb, want_weights, z_f)
         return outputs

@@ -227,10 +227,12 @@ class RenderPoints(torch.autograd.Function):
         lib = _lib.load()
         dev = z.device
         ns = net.num_views_per_obj
-        n_save = lib.pnr_point_save_floats(desc, P * ns)
-        if n_save == 0:
-            _lib.check(-1, "pnr_point_save_floats")
-        save = torch.empty(n_save, dtype=torch.float32, device=dev)
+        save = None
+        if any(ctx.needs_input_grad):   # no activation save without a backward (no_grad)
+            n_save = lib.pnr_point_save_floats(desc, P * ns)
+            if n_save == 0:
+                _lib.check(-1, "pnr_point_save_floats")
+            save = torch.empty(n_save, dtype=torch.float32, device=dev)
         ws_bytes = lib.pnr_point_query_workspace_bytes(sc, P)
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         out = torch.empty(P, 4, dtype=torch.float32, device=dev)

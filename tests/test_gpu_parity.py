@@ -354,7 +354,7 @@ def compare_render(name, out, cfg, arr, max_flips=MAX_FLIPS):
     w = f.weights.reshape(B, -1).cpu()
     assert "z" in f and "z" in c, "render with renderer.return_z = True"
     streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
-    z_exp = parity.expected_fine_z(arr["rays"], c.z, c.weights, c.depth, streams, c.z.shape[-1],
+    z_exp = parity.expected_fine_sets(arr["rays"], c.z, c.weights, c.depth, streams, c.z.shape[-1],
                                    cfg["n_fine"], cfg.get("n_fine_depth", 0), cfg.get("depth_std", 0.01),
                                    cfg.get("lindisp", False))
     cls = parity.classify_fine(c.weights.reshape(B, -1), arr["coarse_weights"].reshape(B, -1),

@@ -58,3 +58,30 @@ def test_classifier_catches_sample_errors():
     bad[flip_ray, 7] += 1e-3        # a flipped ray that does not follow its own weights
     cls = parity.classify_fine(w_hip, w_ref, arr["u_fine"], bad, arr["z_fine"], z_hip)
     assert cls["inconsistent"].nonzero().reshape(-1).tolist() == [flip_ray]
+
+
+def test_marginal_draws_may_take_either_neighbouring_bin():
+    """A draw ON a cdf boundary (fw_shipped's force_u_high rays: u = 1 - 2^-24 against
+    cdf[-1] = 1 +- ulp) may land in either bin from the same weights, because the device
+    sums the normaliser in another order; the alternative set moves exactly those draws, and
+    a sample set that is neither the expected nor the alternative still fails."""
+    cfg, arr = fixtures.load("fw_shipped")
+    B = arr["rays"].reshape(-1, 8).shape[0]
+    w = arr["coarse_weights"].reshape(B, -1)
+    streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
+    args = (arr["rays"], arr["z_coarse"], w, arr["coarse_depth"], streams, cfg["n_coarse"], cfg["n_fine"],
+            cfg["n_fine_depth"], cfg.get("depth_std", 0.01))
+    z0, z1 = parity.expected_fine_sets(*args)
+    marginal = parity.boundary_distance(w, arr["u_fine"]) <= parity.MARGIN
+    moved = (z0 != z1).any(-1)
+    assert int(marginal[: cfg["force_u_high"]].sum()) == cfg["force_u_high"]
+    assert torch.equal(moved, moved & marginal) and bool(moved.any())
+    # a HIP ray that took the other bin of a boundary draw, with flip evidence: consistent
+    flip_w = w.clone()
+    cls = parity.classify_fine(flip_w, w, arr["u_fine"], z1, z0, (z0, z1))
+    assert not cls["inconsistent"].any()
+    # a set that follows neither is inconsistent wherever it is flagged as flipped
+    bad = z1.clone()
+    bad[:, 3] += 1e-2
+    cls = parity.classify_fine(w, w, arr["u_fine"], bad, z0, (z0, z1))
+    assert bool((cls["inconsistent"] == cls["flip"]).all())
