@@ -56,7 +56,7 @@ sys.path.insert(0, REPO)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from pnr import _lib, synth, util  # noqa: E402
+from pnr import _lib, synth, torchops, util  # noqa: E402
 from pnr import dist as pdist  # noqa: E402
 from pnr.models import PRECISIONS, PixelNeRFNet  # noqa: E402
 from pnr.renderer import NeRFRenderer  # noqa: E402
@@ -129,27 +129,23 @@ class HipEvents:
 
 class RenderProbe:
     """Records HIP events around every kernel of each fused render call while `on`
-    (pnr_render_forward_proj's `events` argument: no host synchronization is added), and
-    the call's ray count, so per-launch durations and algorithmic work come from the same
-    launches as the timed region."""
+    (torch.ops.pnr.render_rays' `events` argument, through pnr.torchops.EVENTS_HOOK: no host
+    synchronization is added), and the call's ray count, so per-launch durations and
+    algorithmic work come from the same launches as the timed region."""
 
     def __init__(self, ev):
         self.ev = ev
-        self.lib = _lib.load()
-        self.orig = self.lib.pnr_render_forward_proj
         self.on = False
         self.calls = []      # (events, n_rays, n_coarse, n_fine)
 
-        def render_with_events(*a):
+        def hook(n_rays, n_coarse, n_fine):
             if not self.on:
-                return self.orig(*a)
+                return []
             evs = ev.create(7)
-            rays, cfg = a[6], a[8]
-            self.calls.append((evs, int(rays.n_rays), int(cfg.n_coarse), int(cfg.n_fine)))
-            arr = (ctypes.c_void_p * 7)(*[e.value for e in evs])
-            return self.orig(*a[:-1], arr)
+            self.calls.append((evs, int(n_rays), int(n_coarse), int(n_fine)))
+            return [int(e.value) for e in evs]
 
-        self.lib.pnr_render_forward_proj = render_with_events
+        torchops.EVENTS_HOOK = hook
 
     def reset(self):
         self.calls = []

@@ -456,19 +456,14 @@ class PixelNeRFNet(nn.Module):
             raise ValueError("xyz has %d objects but encode() saw %d" % (SB, self.num_objs))
         from .ops import _dev
 
+        from . import torchops
+
         xyz = _dev(xyz, "xyz")
         vd = _dev(viewdirs.reshape(SB, B, 3), "viewdirs") if viewdirs is not None else None
         desc, packed = self.hip_mlp(coarse)
-        sc = self.hip_scene()
-        proj = self.hip_proj(coarse, sc)
-        lib = _lib.load()
-        ws_bytes = lib.pnr_point_query_workspace_bytes(sc, SB * B)
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=xyz.device)
-        out = torch.empty(SB, B, 4, dtype=torch.float32, device=xyz.device)
-        _lib.check(lib.pnr_point_query_proj(sc, desc, _lib.ptr(packed), _lib.ptr(proj), _lib.ptr(xyz),
-                                            _lib.ptr(vd), B, _lib.ptr(out), _lib.ptr(ws), ws_bytes,
-                                            _lib.stream_of(xyz.device)), "pnr_point_query_proj")
-        return out
+        proj = self.hip_proj(coarse)
+        return torchops.load().point_query(*torchops.scene_args(self), torchops.desc_list(desc), packed, proj,
+                                           xyz, vd)
 
     # ---- checkpoints (models.py:268-316) -------------------------------------------
     def load_weights(self, args, opt_init=False, strict=True, device=None):

@@ -59,16 +59,12 @@ def composite(z, raw, rays, white_bkgd, want_weights=True):
     z = _dev(z, "z")
     raw = _dev(raw, "raw")
     rays = _dev(rays, "rays")
+    from . import torchops
+
     B, K = z.shape
     assert raw.shape[:2] == (B, K) and raw.shape[-1] == 4, raw.shape
-    rgb = torch.empty(B, 3, device=z.device, dtype=torch.float32)
-    depth = torch.empty(B, device=z.device, dtype=torch.float32)
-    w = torch.empty(B, K, device=z.device, dtype=torch.float32) if want_weights else None
-    lib = _lib.load()
-    _lib.check(lib.pnr_composite(_lib.ptr(z), _lib.ptr(raw), _lib.ptr(rays), B, K,
-                                 int(bool(white_bkgd)), _lib.ptr(w), _lib.ptr(rgb), _lib.ptr(depth),
-                                 _lib.stream_of(z.device)), "pnr_composite")
-    return w, rgb, depth
+    w, rgb, depth = torchops.load().composite(z, raw, rays, bool(white_bkgd), bool(want_weights))
+    return (w if want_weights else None), rgb, depth
 
 
 def rng_fill(seed, offset, stream, n_rays, width, device="cuda"):

@@ -278,49 +278,31 @@ class NeRFRenderer(torch.nn.Module):
                        for p in parts[0]})
 
     def _fused_call(self, net, rays, sb, streams, seed, offset, kc, kf, kfd, coarse, want_weights):
-        """One pnr_render_forward_proj call.  coarse=False: the fine MLP in the coarse slot
-        (a coarse-only march with the fine model)."""
+        """One torch.ops.pnr.render_rays call (pnr_render_forward_proj).  coarse=False: the
+        fine MLP in the coarse slot (a coarse-only march with the fine model)."""
+        from . import torchops
+
+        ops_ = torchops.load()
         B = rays.shape[0]
-        dev = rays.device
-        cfg = _lib.RenderCfg(kc, kf, kfd, float(self.depth_std), int(bool(self.white_bkgd)),
-                             int(bool(self.lindisp)))
-        sc = net.hip_scene()
         desc, pc = net.hip_mlp(coarse)
-        _, pf = net.hip_mlp(False) if kf > 0 else (None, None)
-        zc = net.hip_proj(coarse, sc)
-        zf = net.hip_proj(False, sc) if kf > 0 else None
-        f32 = dict(device=dev, dtype=torch.float32)
-        c_rgb, c_depth = torch.empty(B, 3, **f32), torch.empty(B, **f32)
-        c_w = torch.empty(B, kc, **f32) if want_weights or kf > 0 else None
-        f_rgb = torch.empty(B, 3, **f32) if kf > 0 else None
-        f_depth = torch.empty(B, **f32) if kf > 0 else None
-        f_w = torch.empty(B, kc + kf, **f32) if (want_weights and kf > 0) else None
-        z_c = torch.empty(B, kc, **f32) if self.return_z else None
-        z_f = torch.empty(B, kc + kf, **f32) if (self.return_z and kf > 0) else None
-        out = _lib.RenderOut(c_rgb.data_ptr(), c_depth.data_ptr(),
-                             c_w.data_ptr() if c_w is not None else None,
-                             f_rgb.data_ptr() if f_rgb is not None else None,
-                             f_depth.data_ptr() if f_depth is not None else None,
-                             f_w.data_ptr() if f_w is not None else None,
-                             z_c.data_ptr() if z_c is not None else None,
-                             z_f.data_ptr() if z_f is not None else None)
-        r = _lib.Rays(rays.data_ptr(), B, B // sb)
+        pf = net.hip_mlp(False)[1] if kf > 0 else pc
+        zc = net.hip_proj(coarse)
+        zf = net.hip_proj(False) if kf > 0 else None
         if streams is None:
-            rng = _lib.Rng(None, None, None, None, seed, offset)
+            u_c = u_f = u_j = n_d = None
         else:
             u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
-            rng = _lib.Rng(u_c.data_ptr(), u_f.data_ptr() if u_f.numel() else None,
-                           u_j.data_ptr() if u_j.numel() else None,
-                           n_d.data_ptr() if n_d.numel() else None, 0, 0)
-        lib = _lib.load()
-        ws_bytes = lib.pnr_render_workspace_bytes(sc, cfg, B)
-        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
-        _lib.check(lib.pnr_render_forward_proj(sc, desc, _lib.ptr(pc), _lib.ptr(pf), _lib.ptr(zc), _lib.ptr(zf),
-                                               r, rng, cfg, out, _lib.ptr(ws), ws_bytes,
-                                               _lib.stream_of(dev), None), "pnr_render_forward_proj")
-        outputs = DotMap(coarse=self._pack_out(c_w, c_rgb, c_depth, sb, want_weights, z_c))
+        res = ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, pf, zc, zf, rays,
+                               B // sb, kc, kf, kfd, float(self.depth_std), bool(self.white_bkgd),
+                               bool(self.lindisp), u_c, u_f, u_j, n_d, int(seed or 0), int(offset),
+                               bool(want_weights), bool(self.return_z),
+                               torchops.EVENTS_HOOK(B, kc, kf) if torchops.EVENTS_HOOK else [])
+        c_rgb, c_depth, c_w, f_rgb, f_depth, f_w, z_c, z_f = res
+        outputs = DotMap(coarse=self._pack_out(c_w if want_weights else None, c_rgb, c_depth, sb, want_weights,
+                                               z_c if self.return_z else None))
         if kf > 0:
-            outputs.fine = self._pack_out(f_w, f_rgb, f_depth, sb, want_weights, z_f)
+            outputs.fine = self._pack_out(f_w if want_weights else None, f_rgb, f_depth, sb, want_weights,
+                                          z_f if self.return_z else None)
         return outputs
 
     def _forward_callback(self, model, rays, sb, streams, want_weights):

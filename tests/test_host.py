@@ -160,3 +160,25 @@ def test_parser_reads_reference_confs():
         net = PixelNeRFNet(dict(c["model"], encoder=dict(c["model"]["encoder"], pretrained=False)))
         assert net.d_in == 42 and net.mlp_coarse.n_blocks == 5
         assert net.hip_unsupported_reason() == "encode() has not been called"
+
+
+def test_torch_ops_registered_with_meta_shapes():
+    """torch.ops.pnr.{render_rays, point_query, composite} (libpnr_torch.so, TORCH_LIBRARY over
+    the C ABI) load on the CPU host and give their output shapes on meta tensors (FakeTensor /
+    torch.compile tracing) -- no compute without a GPU."""
+    import torch
+
+    from pnr import torchops
+
+    ops = torchops.load()
+    m = dict(device="meta")
+    rays = torch.empty(6, 8, **m)
+    w, rgb, depth = ops.composite(torch.empty(6, 9, **m), torch.empty(6, 9, 4, **m), rays, True, True)
+    assert (w.shape, rgb.shape, depth.shape) == ((6, 9), (6, 3), (6,))
+    lat, cams, pk = torch.empty(1, 32, 32, 512, **m), torch.empty(1, 16, **m), torch.empty(8, **m)
+    desc = [42, 512, 512, 4, 5, 3, 12, 3]
+    out = ops.render_rays(lat, cams, 1, 1, 64.0, 64.0, desc, pk, pk, None, None, rays, 6, 64, 32, 16, 0.01,
+                          True, False, None, None, None, None, 7, 0, True, True)
+    assert [tuple(t.shape) for t in out] == [(6, 3), (6,), (6, 64), (6, 3), (6,), (6, 96), (6, 64), (6, 96)]
+    q = ops.point_query(lat, cams, 1, 1, 64.0, 64.0, desc, pk, None, torch.empty(1, 10, 3, **m), None)
+    assert tuple(q.shape) == (1, 10, 4)
