@@ -77,7 +77,7 @@ typedef struct pnr_mlp_desc {
  *                   (max <= 2^14), each split into two fp16 parts x = x0 + x1 (|x - x0 - x1|
  *                   <= 2^-22 |x|); 3 exact products x0 y0 + x0 y1 + x1 y0 on
  *                   v_mfma_f32_16x16x32_f16, fp32 accumulation, scales undone exactly.
- *                   Error at the fp32 level (scripts/precision_study.py). */
+ *                   Error at the fp32 level (tools/precision_study.py). */
 #define PNR_PREC_F32 0
 #define PNR_PREC_F16X3 3
 #define PNR_PREC_BF16X6 6

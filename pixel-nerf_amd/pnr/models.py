@@ -33,7 +33,7 @@ __all__ = ["PositionalEncoding", "ResnetBlockFC", "ResnetFC", "PixelNeRFNet", "m
 #   "bf16x6" the 6 largest products of that split (error at the fp32 unit roundoff)
 #   "f16x3"  power-of-two scaled operands (per layer / per activation column), each
 #            split into two fp16 parts; 3 exact products on v_mfma_f32_16x16x32_f16
-#            (error at the fp32 level, scripts/precision_study.py)
+#            (error at the fp32 level, tools/precision_study.py)
 PRECISIONS = {"fp32": 0, "f16x3": 3, "bf16x6": 6, "bf16x9": 9}
 
 

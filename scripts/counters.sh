@@ -1,10 +1,10 @@
 #!/bin/bash
-# PMC passes over a probe script (default scripts/mlp_probe.py; one rocprofv3 run per
+# PMC passes over a probe script (default tools/mlp_probe.py; one rocprofv3 run per
 # counter group).  Usage: counters.sh <tag> [probe.py]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 REPO=$(pwd)
 OUT=$REPO/gpurun_out/ctr_${1:-x}
-PROBE=$REPO/${2:-scripts/mlp_probe.py}
+PROBE=$REPO/${2:-tools/mlp_probe.py}
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp

@@ -1,6 +1,7 @@
 #!/bin/bash
-# rocprofv3 kernel-trace stats + separate PMC passes (FETCH_SIZE / WRITE_SIZE) of a
-# short bench run.  Output under gpurun_out/prof_<tag>/.
+# rocprofv3 kernel-trace stats of a short bench run (every leg but the CPU one) + separate
+# PMC passes (FETCH_SIZE / WRITE_SIZE) of the headline cfg3 leg alone (one step).  Output
+# under gpurun_out/prof_<tag>/; scripts/summarize_profile.py <tag> writes profiles/<tag>/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 REPO=$(pwd)
 TAG=${1:-r1}
@@ -10,14 +11,15 @@ export TMPDIR=/tmp
 cd /tmp
 echo "== kernel trace"; date
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 $REPO/bench.py --steps 3 --warmup 1 --no-cpu --no-compare --no-extra > $OUT/trace_bench.log 2>&1
+    python3 $REPO/bench.py --steps 3 --warmup 1 --no-cpu --no-compare --no-extra --no-train > $OUT/trace_bench.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 $OUT/trace_bench.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
 for ctr in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $ctr"; date
   timeout -k 10 600 rocprofv3 --pmc $ctr --output-format csv -d $OUT/pmc_$ctr -o run -- \
-      python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu --no-compare --no-extra > $OUT/pmc_$ctr.log 2>&1
+      python3 $REPO/bench.py --steps 1 --warmup 0 --no-cpu --no-compare --no-extra --no-train --no-cfg2 \
+      --no-composite > $OUT/pmc_$ctr.log 2>&1
   rc=$?; echo "pmc $ctr rc=$rc"
   [ $rc -eq 0 ] || exit $rc
 done
-find $OUT -name "*.csv" | head -20
+du -sh $OUT; find $OUT -name "*.csv" -size +20M -print -delete

@@ -6,7 +6,8 @@
                     and the HBM bytes with the gfx950 correction of MI355X_MICROARCH.md
                     (FETCH_SIZE counts half of wide coalesced streaming reads: x2)
 
-Usage: python scripts/summarize_profile.py <tag> [note]
+Usage: python scripts/summarize_profile.py <tag> [note] [workload]
+(workload labels the PMC rows: the PMC passes of scripts/profile.sh run the cfg3 leg only)
 """
 import csv
 import os
@@ -33,6 +34,7 @@ def kname(full):
 def main():
     tag = sys.argv[1]
     note = sys.argv[2] if len(sys.argv) > 2 else ""
+    workload = sys.argv[3] if len(sys.argv) > 3 else "cfg3"
     src = os.path.join(REPO, "gpurun_out", "prof_" + tag)
     dst = os.path.join(REPO, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
@@ -62,11 +64,11 @@ def main():
     with open(os.path.join(dst, "mlp_dispatch_stats.csv"), "w") as f:
         f.write("# k_point_mlp launches of the kernel-trace run, by render pass\n" + "\n".join(stats) + "\n")
     lines = [
-        "# rocprofv3 PMC summary, %s (bench.py --steps 1 --warmup 0 --no-cpu) %s" % (tag, note),
+        "# rocprofv3 PMC summary, %s (bench.py headline leg only, --steps 1 --warmup 0) %s" % (tag, note),
         "# FETCH_SIZE/WRITE_SIZE in KB as rocprofv3 reports them (per dispatch).",
         "# gfx950: FETCH_SIZE reads 1/2 of wide coalesced streaming reads (MI355X_MICROARCH.md HBM)"
         " -> corrected = 2x.",
-        "kernel,grid,dispatch_ms,FETCH_SIZE_KB,WRITE_SIZE_KB,hbm_bytes_corrected,pass   (kernel names quoted)",
+        "kernel,grid,dispatch_ms,FETCH_SIZE_KB,WRITE_SIZE_KB,hbm_bytes_corrected,pass,workload   (kernel names quoted)",
     ]
     fetch.sort(key=lambda r: int(r["Dispatch_Id"]))
     last = "query"
@@ -84,8 +86,8 @@ def main():
         fk = float(r["Counter_Value"])
         wk = wmap.get(r["Dispatch_Id"], 0.0)
         ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
-        lines.append('"%s",%s,%.4f,%.1f,%.1f,%d,%s' % (name, r["Grid_Size"], ms, fk, wk,
-                                                     int((2 * fk + wk) * 1024), label))
+        lines.append('"%s",%s,%.4f,%.1f,%.1f,%d,%s,%s' % (name, r["Grid_Size"], ms, fk, wk,
+                                                        int((2 * fk + wk) * 1024), label, workload))
     with open(os.path.join(dst, "pmc_summary.csv"), "w") as f:
         f.write("\n".join(lines) + "\n")
     print("wrote", dst)

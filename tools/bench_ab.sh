@@ -1,6 +1,6 @@
 #!/bin/bash
 # bench.py (render line only) for libpnr.so variants in one box session, alternating.
-# Usage: VARIANTS="tagA default" bash scripts/bench_ab.sh
+# Usage: VARIANTS="tagA default" bash tools/bench_ab.sh
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 for round in 1 2; do
   for t in ${VARIANTS:-default}; do

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU session for the training path: NS=1 and NS=3 step benchmarks, then the
-# kernel-trace profile of the NS=1 step (scripts/profile_train.sh).  Stops at the first
+# kernel-trace profile of the NS=1 step (tools/profile_train.sh).  Stops at the first
 # failure; each GPU step has its own time limit.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
@@ -14,4 +14,4 @@ timeout -k 10 300 python scripts/bench_train.py --steps 5 --warmup 2 --views 3 >
 rc=$?; echo "rc=$rc"; tail -2 gpurun_out/bench_train_v3.log | cut -c1-400
 [ $rc -eq 0 ] || exit $rc
 echo "== profile"; date
-bash scripts/profile_train.sh $TAG
+bash tools/profile_train.sh $TAG

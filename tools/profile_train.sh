@@ -11,6 +11,6 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT -
 rc=$?; echo "trace rc=$rc"; tail -2 $OUT/log.txt | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
 # keep the stats and a one-step breakdown; the raw trace is too large to copy back
-python3 $REPO/scripts/train_step_breakdown.py $(find $OUT -name "*kernel_trace.csv" | head -1) 40 > $OUT/step_breakdown.txt
+python3 $REPO/tools/train_step_breakdown.py $(find $OUT -name "*kernel_trace.csv" | head -1) 40 > $OUT/step_breakdown.txt
 find $OUT -name "*kernel_trace.csv" -delete
 head -60 $OUT/step_breakdown.txt

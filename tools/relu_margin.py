@@ -2,7 +2,7 @@
 (diagnostic for the gradient tests: a unit within fp32 rounding of zero can land on the
 other side of the kink in another fp32 evaluation and move every gradient below it).
 
-  python scripts/relu_margin.py [ns] [seed] [--conditioned]
+  python tools/relu_margin.py [ns] [seed] [--conditioned]
 """
 import os
 import sys

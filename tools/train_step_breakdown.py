@@ -1,6 +1,6 @@
 """Per-kernel time of the LAST training step in a rocprofv3 kernel trace of
 scripts/bench_train.py (the step after the last-but-one fine-MLP backward).
-Usage: python scripts/train_step_breakdown.py <run_kernel_trace.csv> [top]"""
+Usage: python tools/train_step_breakdown.py <run_kernel_trace.csv> [top]"""
 import collections
 import csv
 import sys
