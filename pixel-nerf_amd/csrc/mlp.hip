@@ -455,7 +455,10 @@ __device__ __forceinline__ void split3(const f4 &lo, const f4 &hi, bf8 &x0, bf8 
 }
 
 // workgroup barrier that waits only for LDS traffic: a __syncthreads() would also
-// emit s_waitcnt vmcnt(0) and drain the weight prefetch that spans k-steps
+// emit s_waitcnt vmcnt(0) and drain the weight prefetch that spans k-steps.  k_point_mlp
+// uses it for every barrier: no wave there reads global memory another wave of the
+// workgroup wrote (outputs, activation saves and per-wave scratch are written once per
+// address), so global loads in flight (projected rows, biases) cross its barriers.
 __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
@@ -629,25 +632,39 @@ constexpr int H_DIST = PNR_H_DIST;   // f16 weight prefetch distance (row tiles)
                                      // 4 measured 1.7 % faster than 3 (5, 6 slower)
 constexpr int H_DIST_3 = 3;          // k_mlp_bwd and the gather-path forward (training):
                                      // 4 spills there
+// The weight register ring of gemm_f16: row tile t = RTW * ks + r of the layer's stream lives
+// in slot t % slots.  hring_prime issues the first DIST row tiles; gemm_f16_primed runs the
+// layer on a primed ring.  Priming the next layer's ring before the publish that precedes it
+// (k_point_mlp) lets those loads' L2 latency pass under the publish and its LDS-only barriers.
+template <int DIST>
+struct HRing {
+    static constexpr int slots = DIST < RTW ? RTW : 2 * RTW;
+    h8 ra[slots][2];
+};
+
+template <int DIST>
+__device__ __forceinline__ void hring_load(HRing<DIST> &R, const float *__restrict__ wp, int slot, int ks, int r) {
+#ifdef PNR_ABLATE_WSTREAM
+    ks = 0;  // diagnostic: no weight stream
+#endif
+    const float *src = wp + (int64_t)ks * SKS16_FLOATS + r * SRT16_FLOATS;
+    R.ra[slot][0] = *reinterpret_cast<const h8 *>(src);
+    R.ra[slot][1] = *reinterpret_cast<const h8 *>(src + 256);
+}
+
+template <int DIST>
+__device__ __forceinline__ void hring_prime(HRing<DIST> &R, const float *__restrict__ wp) {
+#pragma unroll
+    for (int t = 0; t < DIST; ++t) hring_load(R, wp, t, t / RTW, t % RTW);
+}
+
 template <int NKS, int DIST = H_DIST>
-__device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
-                                         const _Float16 *pb1) {
-    constexpr int H_RING = DIST < RTW ? RTW : 2 * RTW;   // register ring slots
+__device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const float *__restrict__ wp,
+                                                const _Float16 *pb0, const _Float16 *pb1) {
+    constexpr int H_RING = HRing<DIST>::slots;   // register ring slots
     static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
     static_assert(NKS % U == 0, "k-steps");
-    h8 ra[H_RING][2];
-    // row tile t = RTW * ks + r of the layer's stream lives in slot t % H_RING
-    auto loadA = [&](int slot, int ks, int r) {
-#ifdef PNR_ABLATE_WSTREAM
-        ks = 0;  // diagnostic: no weight stream
-#endif
-        const float *src = wp + (int64_t)ks * SKS16_FLOATS + r * SRT16_FLOATS;
-        ra[slot][0] = *reinterpret_cast<const h8 *>(src);
-        ra[slot][1] = *reinterpret_cast<const h8 *>(src + 256);
-    };
-#pragma unroll
-    for (int t = 0; t < DIST; ++t) loadA(t, t / RTW, t % RTW);
     // one k-step; ph = ks % U (static), tail = this is one of the last U k-steps
     auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
         constexpr int ph = decltype(ph_tag)::value;
@@ -661,9 +678,9 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const int tn = ph * RTW + r + DIST;            // prefetch target, relative to the iteration
-            if (!tail || tn < U * RTW) loadA(tn % H_RING, ks - ph + tn / RTW, tn % RTW);
+            if (!tail || tn < U * RTW) hring_load(R, wp, tn % H_RING, ks - ph + tn / RTW, tn % RTW);
             __builtin_amdgcn_sched_barrier(0);
-            const h8 *a = ra[(ph * RTW + r) % H_RING];
+            const h8 *a = R.ra[(ph * RTW + r) % H_RING];
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
                 f4 v = acc[r][c];
@@ -681,6 +698,14 @@ __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp,
 #pragma unroll 1
     for (int ks = 0; ks + U < NKS; ks += U) iter(ks, std::false_type{});
     iter(NKS - U, std::true_type{});
+}
+
+template <int NKS, int DIST = H_DIST>
+__device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
+                                         const _Float16 *pb1) {
+    HRing<DIST> R;
+    hring_prime(R, wp);
+    gemm_f16_primed<NKS, DIST>(acc, R, wp, pb0, pb1);
 }
 
 // 4 (or 8) fp32 values -> scaled fp16 parts written to P0 / P1 at half offset `off`
@@ -899,9 +924,11 @@ __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, 
         }
 }
 
-// hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index)
+// hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index).
+// R: a ring primed (hring_prime) on this layer's weights, or nullptr (PREC 3 only).
 template <int PREC, int NK, int DIST = H_DIST>
-__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx) {
+__device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx,
+                                           HRing<DIST> *R = nullptr) {
     PT(g, 3);
     PT_COUNT(g, 5);
     if constexpr (PREC == 0) {
@@ -922,7 +949,8 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
-        gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
+        if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
+        else gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -998,7 +1026,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #ifndef PNR_GEMM_ONLY
         if constexpr (PREC != 3)
 #endif
-            __syncthreads();
+            lds_barrier();
     };
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (a.save) {
@@ -1018,7 +1046,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
         if constexpr (PREC == 3) {
             relu_colmax(acc, cmax, wave, lane);
-            __syncthreads();
+            lds_barrier();
             relu_store_split(acc, P0, P1, cmax, ecol, wave, lane);
         } else {
             store_relu(acc, inbuf, wave, lane);
@@ -1029,7 +1057,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     if (tid < COLS) ecol[tid] = -8;
     for (int i = tid; i < 2 * PART_HALVES; i += NTHR)   // nonzero operands (power / clock)
         P0[i] = (_Float16)(0.25f + 0.001f * (float)(i % 977));
-    __syncthreads();
+    lds_barrier();
 #endif
     Acc x, h;
     // Dynamic, XCD-aware tile order.  Workgroups are placed round-robin on the 8 XCDs
@@ -1054,7 +1082,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         return (int)T;
     };
     if (tid == 0) *s_next = grab();
-    __syncthreads();
+    lds_barrier();
     for (int64_t tile = *s_next; tile < a.n_tiles; tile = *s_next) {
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         // (addresses formed at use: nothing per tile stays live across the GEMMs)
@@ -1103,7 +1131,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT_WAIT();
             PT(gc, 9);
             // features f = FPT qt .. FPT qt + FPT - 1 of [xyz_rot | PE | viewdir_cam | 0]
-            __syncthreads();   // previous users of inbuf are done
+            lds_barrier();   // previous users of inbuf are done
             PT(gc, 10);
             {
                 const int npe = 3 * L.pe_n;
@@ -1184,7 +1212,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 *reinterpret_cast<f4 *>(t + 4) = f4{wnw, wne, wsw, wse};
             }
             PT(gc, 12);
-            __syncthreads();   // features visible
+            lds_barrier();   // features visible
             PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, lane, false);
@@ -1198,18 +1226,18 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     const float *pz = a.proj + blk * a.proj_stride;
                     ProjRows<PJ> rows;
                     proj_load(rows, pz, gtab, 0, wave, lane);
-                    __syncthreads();
+                    lds_barrier();
                     PT(gc, 3);
                     proj_blend_store(rows, inbuf, 0, wave, lane);
                     ProjRows<PJ2> rows2;
                     proj_load(rows2, pz, gtab, PJ, wave, lane);
                     proj_blend_store(rows2, inbuf, PJ, wave, lane);
-                    __syncthreads();
+                    lds_barrier();
                     PT(gc, 1);
                     add_bias(x, bias + (1 + lz) * H, wave, lane, true);
                     add_stage(x, inbuf, wave, lane);
                 } else {
-                __syncthreads();
+                lds_barrier();
                 PT(gc, 3);
                 // z = bilinear latent gather (torch's nw, ne, sw, se summation order).
                 // Wave w walks its COLS / WAVES columns; each load instruction reads one
@@ -1259,23 +1287,31 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                         if (lane == 0) ecol[cj] = e;
                     }
                 }
-                __syncthreads();
+                lds_barrier();
                 PT(gc, 1);
                 add_bias(x, bias + (1 + lz) * H, wave, lane, true);
                 layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 pre_publish_sync();
                 }
+                HRing<KD> R0;   // fc_0's ring, primed before the publish (PREC 3)
+                if constexpr (PREC == 3)
+                    hring_prime(R0, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
                 publish_relu(x, tile, blk, v * P);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
-                __syncthreads();
+                lds_barrier();
                 add_bias(h, bias + (2 + lz) * H, wave, lane, false);
-                layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz);
+                layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
+                                          PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
+                HRing<KD> R1;   // fc_1's
+                if constexpr (PREC == 3)
+                    hring_prime(R1, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off));
                 publish_relu(h, tile, L.n_blocks + blk, v * P);
-                __syncthreads();
+                lds_barrier();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
                 add_bias(x, bias + (3 + lz) * H, wave, lane, true);
-                layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz);
+                layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
+                                          PREC == 3 ? &R1 : nullptr);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -1310,23 +1346,31 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         for (int blk = L.ncomb; blk < L.n_blocks; ++blk) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             pre_publish_sync();
+            HRing<KD> R0;
+            if constexpr (PREC == 3)
+                hring_prime(R0, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off));
             publish_relu(x, tile, blk, 0);
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
-            __syncthreads();
+            lds_barrier();
             add_bias(h, bias + (1 + l0) * H, wave, lane, false);
-            layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0);
+            layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
+                                      PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
+            HRing<KD> R1;
+            if constexpr (PREC == 3)
+                hring_prime(R1, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
             publish_relu(h, tile, L.n_blocks + blk, 0);
-            __syncthreads();
+            lds_barrier();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
             add_bias(x, bias + (2 + l0) * H, wave, lane, true);
-            layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0);
+            layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
+                                      PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = grab();   // read after the barrier closing this iteration
         pre_publish_sync();
         publish_relu(x, tile, 2 * L.n_blocks, 0);
-        __syncthreads();
+        lds_barrier();
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY
         if (0)
@@ -1385,7 +1429,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
         PT(gc, 4);
         PT_COUNT(gc, 6);
-        __syncthreads();   // s_next and the head partials written
+        lds_barrier();   // s_next and the head partials written
         if (PREC == 3 && wave < CT) {   // [sigmoid(rgb), relu(sigma)] of column tile `wave`
             const int ln = opaque_lane(lane), gg = ln >> 4, cc = ln & 15;
             const f4 h0 = *reinterpret_cast<const f4 *>(hpart + (wave * 64 + ln) * 4);

@@ -25,6 +25,6 @@ for f in march.hip mlp.hip train.hip encoder.hip wgrad.hip proj.hip abi.cpp; do
   objs+=("$out/$f.o")
 done
 wait
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libpnr.so" "${objs[@]}" \
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libpnr.so" "${objs[@]}" -Wl,-soname,libpnr.so \
   -Wl,-rpath,/opt/rocm/lib
 echo "built $out/libpnr.so"
