@@ -764,6 +764,19 @@ __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _
     }
 }
 
+// this wave's rows of a bias vector (loaded ahead of use: the loads cross LDS-only barriers)
+__device__ __forceinline__ void load_bias(f4 (&b)[RTW], const float *__restrict__ bias, int wave, int lane) {
+    const int g = opaque_lane(lane) >> 4;
+#pragma unroll
+    for (int r = 0; r < RTW; ++r) b[r] = *reinterpret_cast<const f4 *>(bias + 16 * (RTW * wave + r) + 4 * g);
+}
+__device__ __forceinline__ void set_bias(Acc &acc, const f4 (&b)[RTW], bool accumulate) {
+#pragma unroll
+    for (int r = 0; r < RTW; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[r][c] = accumulate ? acc[r][c] + b[r] : b[r];
+}
+
 // acc = bias (per output row) [+ acc]
 __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bias, int wave, int lane,
                                          bool accumulate) {
@@ -1296,20 +1309,25 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 HRing<KD> R0;   // fc_0's ring, primed before the publish (PREC 3)
                 if constexpr (PREC == 3)
                     hring_prime(R0, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                f4 nb0[RTW];
+                load_bias(nb0, bias + (2 + lz) * H, wave, lane);
+#endif
                 publish_relu(x, tile, blk, v * P);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 lds_barrier();
-                add_bias(h, bias + (2 + lz) * H, wave, lane, false);
+                set_bias(h, nb0, false);
                 layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
                                           PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
                 if constexpr (PREC == 3)
                     hring_prime(R1, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                f4 nb1[RTW];
+                load_bias(nb1, bias + (3 + lz) * H, wave, lane);
                 publish_relu(h, tile, L.n_blocks + blk, v * P);
                 lds_barrier();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
-                add_bias(x, bias + (3 + lz) * H, wave, lane, true);
+                set_bias(x, nb1, true);
                 layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
                                           PREC == 3 ? &R1 : nullptr);
             }
@@ -1349,20 +1367,24 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             HRing<KD> R0;
             if constexpr (PREC == 3)
                 hring_prime(R0, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off));
+            f4 nb0[RTW];
+            load_bias(nb0, bias + (1 + l0) * H, wave, lane);
             publish_relu(x, tile, blk, 0);
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
             lds_barrier();
-            add_bias(h, bias + (1 + l0) * H, wave, lane, false);
+            set_bias(h, nb0, false);
             layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
                                       PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
             HRing<KD> R1;
             if constexpr (PREC == 3)
                 hring_prime(R1, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
+            f4 nb1[RTW];
+            load_bias(nb1, bias + (2 + l0) * H, wave, lane);
             publish_relu(h, tile, L.n_blocks + blk, 0);
             lds_barrier();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
-            add_bias(x, bias + (2 + l0) * H, wave, lane, true);
+            set_bias(x, nb1, true);
             layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
                                       PREC == 3 ? &R1 : nullptr);
         }
@@ -1374,7 +1396,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY
         if (0)
-#endif
         if (PREC == 3) {
             // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col, the k range
             // split over the 8 waves: wave w sums column tile w % 4 over k-half w / 4 into LDS;
