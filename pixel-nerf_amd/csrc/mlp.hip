@@ -1309,9 +1309,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 HRing<KD> R0;   // fc_0's ring, primed before the publish (PREC 3)
                 if constexpr (PREC == 3)
                     hring_prime(R0, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
-                f4 nb0[RTW];
+                f4 nb0[RTW];   // fc_0's bias rows, loaded before the publish too
                 load_bias(nb0, bias + (2 + lz) * H, wave, lane);
-#endif
                 publish_relu(x, tile, blk, v * P);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 lds_barrier();
@@ -1396,6 +1395,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY
         if (0)
+#endif
         if (PREC == 3) {
             // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col, the k range
             // split over the 8 waves: wave w sums column tile w % 4 over k-half w / 4 into LDS;
