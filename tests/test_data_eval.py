@@ -137,6 +137,65 @@ def test_eval_approx_end_to_end(tmp_path):
     assert abs(p0 - res["psnr"][0]) < 1e-5
 
 
+
+@pytest.mark.gpu
+def test_eval_approx_psnr_matches_oracle(tmp_path):
+    """pnr.evaluate.eval_approx against the oracle restatement of eval_approx.py's scoring
+    loop (oracle/eval_ref.py): the same encoded latent, rays and counter-mode draws (replayed
+    from the renderer's seed through oracle/philox.py) rendered by the CPU oracle; every
+    object's PSNR agrees within 0.01 dB (the north star's PSNR bar)."""
+    from oracle import eval_ref, philox
+    from pnr import synth
+    from pnr.models import PixelNeRFNet
+    from pnr.renderer import NeRFRenderer
+
+    g = _golden()
+    root = write_srn_dir(str(tmp_path), g)
+    dset = SRNDataset(root, stage="test", image_size=(16, 16))
+    dev = torch.device("cuda", 0)
+    mlp = dict(type="resnet", n_blocks=5, d_hidden=512, combine_layer=3, combine_type="average")
+    conf = dict(use_encoder=True, use_xyz=True, use_code=True, code=dict(num_freqs=6, freq_factor=1.5),
+                use_viewdirs=True, use_code_viewdirs=False, mlp_coarse=mlp, mlp_fine=mlp,
+                encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
+    torch.manual_seed(0)
+    sd = synth.pixelnerf_state(2)
+    net = PixelNeRFNet(conf)
+    net.load_state_dict(sd, strict=False)
+    net = net.to(dev).eval()
+    rec = []
+    enc = net.encode
+
+    def encode(images, poses, focal, *a, **k):
+        rec.append(dict(poses=poses.cpu(), focal=focal.cpu(), images=images.cpu()))
+        return enc(images, poses, focal, *a, **k)
+
+    net.encode = encode
+
+    class RecRenderer(NeRFRenderer):
+        def forward(self, model, rays, want_weights=False):
+            out = super().forward(model, rays, want_weights)
+            rec[-1].update(rays=rays.cpu(), seed=self.last_seed, latent=model.encoder.latent.detach().cpu())
+            return out
+
+    r = RecRenderer(n_coarse=32, n_fine=16, white_bkgd=True).to(dev)
+    res = evaluate.eval_approx(net, r, dset, dev, source=[1], batch_size=2, seed=7)
+    assert r.rng_mode == "counter" and len(rec) == 1
+    b = rec[0]
+    SB, HW = b["rays"].shape[:2]
+    streams = tuple(torch.from_numpy(a) for a in philox.render_streams(b["seed"], 0, SB * HW, 64, 16, 0))
+    # the ground truth as eval_approx picks it (same seed, same draws)
+    torch.random.manual_seed(7)
+    data = next(iter(torch.utils.data.DataLoader(dset, batch_size=2, shuffle=False)))
+    src, dst = evaluate.select_views(2, data["images"].shape[1], [1])
+    from pnr import util
+
+    gt = util.batched_index_select_nd(data["images"] * 0.5 + 0.5, dst).reshape(SB, 3, 16, 16).permute(0, 2, 3, 1)
+    ps, _ = eval_ref.score_batch(sd, b["latent"], b["poses"].reshape(SB, 1, 4, 4), b["focal"], 16, 16,
+                                 b["rays"], streams, gt, 64, 16)
+    np.testing.assert_allclose(res["psnr"], ps, rtol=0, atol=0.01)
+    print("eval_approx PSNR hip %s oracle %s" % (res["psnr"], ps))
+
+
 CLI_CONF = """
 model {
     use_encoder = True
