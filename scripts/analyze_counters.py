@@ -11,6 +11,9 @@ prints the mean over launches of:
                  as fractions of SQ_WAVE_CYCLES (MI355X_MICROARCH.md: disjoint, sum ~ 1)
   lds_conflict   SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
   l2_hit         TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
+  l2_req_gb      (TCC_HIT_sum + TCC_MISS_sum) x 128 B: L2 requests of the launch (CU reads
+                 of 16 B/lane coalesced rows arrive as 128-B line requests)
+  hbm_gb         FETCH_SIZE x 2 (KB; gfx950 correction of MI355X_MICROARCH.md), when collected
 """
 import csv
 import glob
@@ -72,6 +75,9 @@ def main():
             line.append("lds_conflict %.3f" % (m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]))
         if "TCC_HIT_sum" in m:
             line.append("l2_hit %.4f" % (m["TCC_HIT_sum"] / (m["TCC_HIT_sum"] + m["TCC_MISS_sum"])))
+            line.append("l2_req_gb %.1f" % ((m["TCC_HIT_sum"] + m["TCC_MISS_sum"]) * 128e-9))
+        if "FETCH_SIZE" in m:
+            line.append("hbm_gb %.2f" % (m["FETCH_SIZE"] * 2 * 1024e-9))
         if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
             line.append("valu/mfma %.2f" % (m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"]))
         print("  ".join(line))

@@ -1,5 +1,5 @@
 #!/bin/bash
-# rocprofv3 kernel-trace stats of a short bench run (every leg but the CPU one) + separate
+# rocprofv3 kernel-trace stats of a short bench run of the headline cfg3 leg alone + separate
 # PMC passes (FETCH_SIZE / WRITE_SIZE) of the headline cfg3 leg alone (one step).  Output
 # under gpurun_out/prof_<tag>/; scripts/summarize_profile.py <tag> writes profiles/<tag>/.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
@@ -11,7 +11,8 @@ export TMPDIR=/tmp
 cd /tmp
 echo "== kernel trace"; date
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 $REPO/bench.py --steps 3 --warmup 1 --no-cpu --no-compare --no-extra --no-train > $OUT/trace_bench.log 2>&1
+    python3 $REPO/bench.py --steps 3 --warmup 1 --no-cpu --no-compare --no-extra --no-train --no-cfg2 \
+    --no-composite > $OUT/trace_bench.log 2>&1
 rc=$?; echo "trace rc=$rc"; tail -3 $OUT/trace_bench.log | cut -c1-300
 [ $rc -eq 0 ] || exit $rc
 for ctr in FETCH_SIZE WRITE_SIZE; do
