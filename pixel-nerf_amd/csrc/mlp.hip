@@ -919,6 +919,98 @@ __device__ __forceinline__ void proj_blend_store(const ProjRows<N> &R, float *st
     }
 }
 static_assert(PJ > 0 && PJ2 > 0, "two batches cover a wave's columns");
+
+// Run-deduplicated stage (PNR_PROJ_RUNS, the default).  A wave's 8 columns are consecutive
+// samples of one ray, and consecutive samples mostly project into the same latent cell
+// (cfg3: 2.1 runs of equal cell per 8 columns, cfg2: 4.9): the 4 corner rows of a run are
+// loaded ONCE and blended with each of its columns' weights (the blend arithmetic per column
+// is unchanged).  Three register slots (96 VGPRs, the two-batch stage holds 128) rotate over
+// the runs: runs 0-2 are issued before the barrier that frees the stage, run k + 3 as soon
+// as run k's columns are blended.  The run pattern is wave-uniform (SGPR bit mask), so every
+// branch below is a scalar branch.
+#ifndef PNR_PROJ_RUNS
+#define PNR_PROJ_RUNS 1
+#endif
+struct CellRows {
+    f4 c[2][4];   // [channel half][corner nw, ne, sw, se]
+};
+__device__ __forceinline__ void cell_load(CellRows &C, const float *__restrict__ pz, const float *gtab, int cj,
+                                          int lane) {
+    const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
+        C.c[half][0] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.x) + ch);
+        C.c[half][1] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.y) + ch);
+        C.c[half][2] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.z) + ch);
+        C.c[half][3] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.w) + ch);
+    }
+}
+__device__ __forceinline__ void cell_blend_store(const CellRows &C, const float *gtab, float *stage, int cj,
+                                                 int lane) {
+    const f4 tw = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
+        const f4 *c = C.c[half];
+        f4 zz;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            zz[q] = add_rn(add_rn(add_rn(mul_rn(c[0][q], tw.x), mul_rn(c[1][q], tw.y)), mul_rn(c[2][q], tw.z)),
+                           mul_rn(c[3][q], tw.w));
+        *reinterpret_cast<f4 *>(stage + cj * LDS_LD + ch) = zz;
+    }
+}
+// bit j set: column c0 + j starts a run (its nw corner offset, which fixes all four corners,
+// differs from column c0 + j - 1's); bit 0 always set
+__device__ __forceinline__ uint32_t cell_run_starts(const float *gtab, int c0) {
+    uint32_t starts = 1u;
+    uint32_t prev = __builtin_amdgcn_readfirstlane(__float_as_uint(gtab[c0 * 8]));
+#pragma unroll
+    for (int j = 1; j < COLS / WAVES; ++j) {
+        const uint32_t k = __builtin_amdgcn_readfirstlane(__float_as_uint(gtab[(c0 + j) * 8]));
+        if (k != prev) starts |= 1u << j;
+        prev = k;
+    }
+    return starts;
+}
+// the whole stage of one wave, including the barrier that frees the image it aliases
+__device__ __forceinline__ void stage_proj_runs(const float *__restrict__ pz, const float *gtab, float *stage,
+                                                int wave, int lane) {
+    constexpr int NC = COLS / WAVES;
+    const int c0 = NC * wave;
+    const uint32_t starts = cell_run_starts(gtab, c0);
+    // first run start after column j (NC = none)
+    auto next = [&](int j) -> int {
+        const uint32_t m = starts & ~((2u << j) - 1u);
+        return m ? __builtin_ctz(m) : NC;
+    };
+    CellRows A, B, C;
+    int a = 0, b = next(0), c = b < NC ? next(b) : NC;
+    cell_load(A, pz, gtab, c0 + a, lane);
+    if (b < NC) cell_load(B, pz, gtab, c0 + b, lane);
+    if (c < NC) cell_load(C, pz, gtab, c0 + c, lane);
+    lds_barrier();   // the previous GEMM's image reads are done: the stage may overwrite it
+    int j = 0;
+    for (;;) {
+        // A holds the run [a, b), B [b, c), C [c, d)
+        const int d = c < NC ? next(c) : NC;
+        for (; j < b; ++j) cell_blend_store(A, gtab, stage, c0 + j, lane);
+        if (j >= NC) break;
+        if (d < NC) cell_load(A, pz, gtab, c0 + d, lane);
+        const int e = d < NC ? next(d) : NC;
+        for (; j < c; ++j) cell_blend_store(B, gtab, stage, c0 + j, lane);
+        if (j >= NC) break;
+        if (e < NC) cell_load(B, pz, gtab, c0 + e, lane);
+        const int f = e < NC ? next(e) : NC;
+        for (; j < d; ++j) cell_blend_store(C, gtab, stage, c0 + j, lane);
+        if (j >= NC) break;
+        if (f < NC) cell_load(C, pz, gtab, c0 + f, lane);
+        a = d;
+        b = e;
+        c = f;
+    }
+}
 static_assert(sizeof(float) * COLS * LDS_LD <= 2 * sizeof(_Float16) * PART_HALVES,
               "the fp32 stage fits in the split image it aliases");
 // x[r][c] += stage rows of this wave (column 16c + cl, rows 16 (RTW wave + r) + 4g ..)
@@ -1237,6 +1329,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     // the stage aliases the image the previous GEMM read; publish_relu's
                     // internal barrier orders the add_stage reads before the image writes
                     const float *pz = a.proj + blk * a.proj_stride;
+#if PNR_PROJ_RUNS && !defined(PNR_ABLATE_GATHER)
+                    stage_proj_runs(pz, gtab, inbuf, wave, lane);
+                    PT(gc, 3);
+#else
                     ProjRows<PJ> rows;
                     proj_load(rows, pz, gtab, 0, wave, lane);
                     lds_barrier();
@@ -1245,6 +1341,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     ProjRows<PJ2> rows2;
                     proj_load(rows2, pz, gtab, PJ, wave, lane);
                     proj_blend_store(rows2, inbuf, PJ, wave, lane);
+#endif
                     lds_barrier();
                     PT(gc, 1);
                     add_bias(x, bias + (1 + lz) * H, wave, lane, true);
