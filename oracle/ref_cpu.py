@@ -51,8 +51,14 @@ def positional_encoding(x, freqs, phases):
     return torch.cat((x, embed), dim=-1)
 
 
-def resnetfc_forward(sd, prefix, zx, d_latent, n_blocks, combine_layer, inner_dims):
-    """resnetfc.py:132-184; blocks are x + fc_1(relu(fc_0(relu(x)))) (53-62)."""
+def resnetfc_forward(sd, prefix, zx, d_latent, n_blocks, combine_layer, inner_dims, relu=None):
+    """resnetfc.py:132-184; blocks are x + fc_1(relu(fc_0(relu(x)))) (53-62).
+
+    ``relu(t, site)`` (tests only) replaces torch.relu at each ReLU: site ("x", b) before
+    block b's fc_0, ("h", b) before its fc_1, ("xf", n_blocks) before lin_out."""
+    if relu is None:
+        def relu(t, site):
+            return torch.relu(t)
 
     def lin(name, t):
         return F.linear(t, sd[prefix + name + ".weight"], sd[prefix + name + ".bias"])
@@ -65,10 +71,10 @@ def resnetfc_forward(sd, prefix, zx, d_latent, n_blocks, combine_layer, inner_di
             x = combine_interleaved(x, inner_dims)
         if d_latent > 0 and blk < combine_layer:
             x = x + lin("lin_z.%d" % blk, z)
-        net = lin("blocks.%d.fc_0" % blk, torch.relu(x))
-        dx = lin("blocks.%d.fc_1" % blk, torch.relu(net))
+        net = lin("blocks.%d.fc_0" % blk, relu(x, ("x", blk)))
+        dx = lin("blocks.%d.fc_1" % blk, relu(net, ("h", blk)))
         x = x + dx
-    return lin("lin_out", torch.relu(x))
+    return lin("lin_out", relu(x, ("xf", n_blocks)))
 
 
 def encode_buffers(poses, focal, width, height, c=None):
@@ -135,9 +141,11 @@ class Scene:
 
 
 def pixelnerf_forward(sd, scene, xyz, coarse=True, viewdirs=None, d_latent=512,
-                      n_blocks=5, combine_layer=3, has_fine=True):
+                      n_blocks=5, combine_layer=3, has_fine=True, relu=None):
     """models.py:146-266 for the shipped conf (use_xyz, normalize_z, use_code,
-    use_viewdirs, use_code_viewdirs=False, no global encoder)."""
+    use_viewdirs, use_code_viewdirs=False, no global encoder).  MLP rows before
+    combine_layer are (object, view, point), after it (object, point); ``relu`` as
+    resnetfc_forward."""
     SB, B, _ = xyz.shape
     NS = scene.ns
     poses = scene.poses
@@ -157,7 +165,7 @@ def pixelnerf_forward(sd, scene, xyz, coarse=True, viewdirs=None, d_latent=512,
     latent = latent.transpose(1, 2).reshape(-1, d_latent)
     mlp_input = torch.cat((latent, z_feature), dim=-1)
     prefix = "mlp_coarse." if (coarse or not has_fine) else "mlp_fine."
-    out = resnetfc_forward(sd, prefix, mlp_input, d_latent, n_blocks, combine_layer, (NS, B))
+    out = resnetfc_forward(sd, prefix, mlp_input, d_latent, n_blocks, combine_layer, (NS, B), relu=relu)
     out = out.reshape(-1, B, 4)
     out = torch.cat([torch.sigmoid(out[..., :3]), torch.relu(out[..., 3:4])], dim=-1)
     return out.reshape(SB, B, -1)

@@ -144,6 +144,105 @@ def test_training_step_multiview_gradients_match_oracle(precision, tol):
     compare(cs, precision, tol)
 
 
+def capture_saves(monkeypatch):
+    """Record the activation save of every RenderPoints forward (pnr/train.py) by pass."""
+    from pnr import train
+
+    caps = {}
+    orig = train.RenderPoints.forward
+
+    def forward(ctx, net, coarse, rays, z, latent_cl, *params):
+        out = orig(ctx, net, coarse, rays, z, latent_cl, *params)
+        save = ctx.to_save[3]   # save_for_backward(rays, z, out, save, latent_cl)
+        caps[bool(coarse)] = dict(save=save.detach().clone(), P=z.numel(), ns=net.num_views_per_obj,
+                                  nb=ctx.mlp.n_blocks, nc=ctx.mlp.combine_layer)
+        return out
+
+    monkeypatch.setattr(train.RenderPoints, "forward", staticmethod(forward))
+    return caps
+
+
+def margin_relu(caps, sb, margin_rel, stats):
+    """ReLU-margin masking: the oracle's ReLU decides a unit itself unless its input is within
+    margin_rel * max|input| of the kink, where it takes the HIP forward's decision (its saved
+    relu output > 0).  Inside that band either side is a valid fp32 outcome; everywhere else
+    a HIP mask that differs from the oracle's is a gradient error the comparison catches."""
+    from pnr import train
+
+    def for_pass(coarse):
+        c = caps[coarse]
+        P, ns, nb = c["P"], c["ns"], c["nb"]
+        nc = min(c["nc"], nb) if ns > 1 else nb
+        _, _, slot = train._save_views(c["save"], P, nb, ns=ns)
+
+        def hip_mask(i, rows):
+            m = (slot(i, rows) > 0).cpu()
+            if rows == ns * P and ns > 1:   # HIP rows (view, object, point) -> oracle (object, view, point)
+                m = m.reshape(ns, sb, P // sb, -1).transpose(0, 1).reshape(rows, -1)
+            return m
+
+        def relu(t, site):
+            kind, b = site
+            if kind == "xf":
+                hip = hip_mask(2 * nb, P)
+            else:
+                rows = ns * P if b < nc else P
+                hip = hip_mask(b if kind == "x" else nb + b, rows)
+            assert hip.numel() == t.numel() and hip.shape[-1] == t.shape[-1], (site, hip.shape, t.shape)
+            hip = hip.reshape(t.shape)   # after combine_layer the oracle's x is (objects, points, 512)
+            band = t.detach().abs() < margin_rel * float(t.detach().abs().max())
+            own = t.detach() > 0
+            stats["band"] += int(band.sum())
+            stats["adopted"] += int((band & (hip != own)).sum())
+            stats["outside"] += int((~band & (hip != own)).sum())
+            return t * torch.where(band, hip, own).to(t.dtype)
+
+        return relu
+
+    return {True: for_pass(True), False: for_pass(False)}
+
+
+@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("f16x3", 2e-4)])
+def test_training_step_multiview_unconditioned_relu_margin(precision, tol, monkeypatch):
+    """SB = 2 x NS = 2 on the hash weights as drawn (no `conditioned` weights): ReLU units
+    within 1e-4 of their layer's max |input| of the kink take the HIP forward's mask in the
+    oracle (ReLU-margin masking, margin_relu); every other mask is the oracle's own, and all
+    gradients are held to the same tolerance as the conditioned test."""
+    torch.set_num_threads(8)
+    cs = case(ns=2)
+    caps = capture_saves(monkeypatch)
+    loss, got = hip_grads(cs, precision)
+    stats = dict(band=0, adopted=0, outside=0)
+    relus = margin_relu(caps, cs["rays"].shape[0], 1e-4, stats)
+
+    sd = dict(cs["sd"])
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith("mlp_")}
+    sd.update(params)
+    latent = cs["latent"].clone().requires_grad_(True)
+    scene = ref_cpu.Scene(latent, cs["poses"], cs["focal"], cs["width"], cs["height"], cs["c"])
+
+    def model_fn(pts, coarse, dirs):
+        return ref_cpu.pixelnerf_forward(sd, scene, pts, coarse, dirs, relu=relus[bool(coarse)])
+
+    out = ref_cpu.render(model_fn, cs["rays"], cs["kc"], cs["kf"], cs["kfd"], cs["streams"], True,
+                         depth_std=0.05)
+    mse = torch.nn.functional.mse_loss
+    ref_loss = mse(out["coarse"]["rgb"], cs["target"]) + mse(out["fine"]["rgb"], cs["target"])
+    ref_loss.backward()
+    ref = {k: p.grad for k, p in params.items()}
+    ref["latent"] = latent.grad
+    print("relu margin band %(band)d units, HIP decision adopted for %(adopted)d, "
+          "masks differing outside the band %(outside)d" % stats)
+    assert stats["outside"] == 0, stats
+    assert abs(loss - ref_loss.item()) <= 1e-5 * abs(ref_loss.item()), (loss, ref_loss.item())
+    assert set(ref) == set(got), set(ref) ^ set(got)
+    for k in sorted(ref):
+        a, b = got[k].reshape(-1).double(), ref[k].reshape(-1).double()
+        scale = float(b.abs().max())
+        err = float((a - b).abs().max())
+        assert err <= tol * scale + 1e-9, "%s: max |d| %.3g vs max |ref| %.3g" % (k, err, scale)
+
+
 def test_training_noise_std_draw_order_matches_reference():
     """noise_std > 0 in training mode (nerf.py:225-226): sigma noise per pass, with the
     reference's draw order u_coarse, coarse noise, u_fine, u_fine_jit, n_depth, fine noise."""
