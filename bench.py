@@ -90,6 +90,7 @@ RAY_BATCH = 50000              # gen_video.py --ray_batch_size default (args.py:
 # cfg2: SRN 128x128 frame in 4096-ray chunks
 CHUNK = 4096
 W = H = 128
+FUSED_MARCH = True   # pnr_render_set_fused(2) (main: --unfused / --fused-mode)
 KERNELS = ["sample_coarse", "mlp_coarse", "composite_coarse", "sample_fine", "mlp_fine", "composite_fine"]
 
 
@@ -165,7 +166,9 @@ class RenderProbe:
         ms = avg["mlp_fine"]
         achieved = flop / (ms * 1e-3) / 1e12
         peak, terms = PEAK_BY_PRECISION[precision]
-        kname = "k_point_mlp<%d, %s>" % (PRECISIONS[precision], "true" if latent_proj else "false")
+        # the fine pass (K = 128) runs the fused-march instantiation unless --unfused
+        kname = "k_point_mlp<%d, %s, %s>" % (PRECISIONS[precision], "true" if latent_proj else "false",
+                                             "true" if FUSED_MARCH else "false")
         return avg, {
             "kernel": "k_point_mlp (fine pass)", "bound": "mfma",
             "achieved": round(achieved, 2), "peak": round(peak, 1),
@@ -661,7 +664,16 @@ def main():
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
     ap.add_argument("--no-latent-proj", action="store_true",
                     help="per-point lin_z GEMMs on the gathered latent (A/B against the projection)")
+    ap.add_argument("--unfused", action="store_true",
+                    help="separate sample / MLP / composite kernels instead of the fused ray march (A/B)")
+    ap.add_argument("--fused-mode", type=int, default=2,
+                    help="pnr_render_set_fused: 2 fused passes + fine-draw kernel (default), 1 fine draws "
+                         "in the coarse epilogue too")
     args = ap.parse_args()
+    global FUSED_MARCH
+    FUSED_MARCH = not args.unfused
+    if hasattr(_lib.load(), "pnr_render_set_fused"):   # absent only in A/B builds of older revisions
+        _lib.load().pnr_render_set_fused(0 if args.unfused else args.fused_mode)
 
     rank, world, local = pdist.init_from_env("nccl")   # RCCL on ROCm; control plane only
     torch.cuda.set_device(local)
@@ -688,6 +700,10 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "arithmetic": ARITHMETIC[args.precision],
+        "march": ("separate sample / MLP / composite kernels" if args.unfused else
+                  "fused (mode %d): one k_point_mlp launch per pass, coarse draws in its prologue, the "
+                  "composite in its epilogue (roofline.launch_ms includes them); fine draws %s"
+                  % (args.fused_mode, "in the coarse epilogue" if args.fused_mode == 1 else "in their own kernel")),
         "data": "synthetic (hash-initialised ResnetFC weights, random-init ResNet34 encoder on a hashed "
                 "64x64 source image; NMR geometry)",
         "config": {"workload": "cfg3: ShapeNet-NMR 64x64, 1 source view, 24 frames = 98,304 rays per step "

@@ -187,7 +187,10 @@ int pnr_render_forward(const pnr_scene *scene, const pnr_mlp_desc *desc,
  * (= before the coarse point MLP), [2] after the coarse MLP, [3] after the coarse
  * composite, [4] after sample_fine, [5] after the fine MLP, [6] after the fine
  * composite (entries 4-6 unused when n_fine == 0).  `events` holds 7 hipEvent_t;
- * no host synchronization is added.  Used by bench.py for per-kernel timing. */
+ * no host synchronization is added.  Used by bench.py for per-kernel timing.
+ * With the fused ray march (pnr_render_set_fused) a pass is one launch: [1]-[2] and
+ * [4]-[5] then time the whole coarse / fine pass (sampling and composite included),
+ * and the other intervals are empty. */
 int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
                               const void *coarse_packed, const void *fine_packed,
                               const pnr_rays *rays, const pnr_rng *rng,
@@ -228,6 +231,17 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc,
                             const pnr_render_cfg *cfg, const pnr_render_out *out,
                             void *workspace, size_t workspace_bytes, pnr_stream_t stream,
                             void *const *events);
+
+/* Fused ray march.  2 (the default): each pass of pnr_render_forward* is one k_point_mlp launch
+ * that draws the coarse depths in its prologue and composites each ray from LDS in its
+ * epilogue (the per-point rgb/sigma never reach HBM); the fine draws (inverse CDF + sort) run
+ * in their own small kernel between the passes.  1: the coarse epilogue draws the fine samples
+ * too (one launch per pass; measured 0.3-0.5 % slower on MI355X, since one wave runs them while
+ * the workgroup's other seven wait).  0: the separate sample / MLP / composite kernels.  The
+ * fusion applies when a pass's samples per ray are 64 or 128 (and kc + kf <= 128 for the fine
+ * draws) and mlp_fine is not None; other shapes take the separate kernels.  All modes run the
+ * same device code and give bit-identical results.  Process-wide; returns the previous setting. */
+int32_t pnr_render_set_fused(int32_t on);
 
 /* ---- building blocks (also the generic model-callback path) ------------------ */
 /* Replaces: NeRFRenderer.sample_coarse (nerf.py:98-118).  z (n_rays, n_coarse). */

@@ -6,7 +6,7 @@
 #include <cstdio>
 #include <cstring>
 
-#include "pnr_common.h"
+#include "march_dev.h"
 
 namespace pnr {
 
@@ -43,11 +43,17 @@ int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, in
                          float *, hipStream_t);
 int launch_point_mlp(const pnr_scene &, const pnr_mlp_desc &, const void *, const float *,
                      const float *, int, int64_t, const float *, const float *, int64_t, int64_t,
-                     float *, float *, hipStream_t, float *save = nullptr, const float *proj = nullptr);
+                     float *, float *, hipStream_t, float *save = nullptr, const float *proj = nullptr,
+                     const MarchCfg *march = nullptr);
+int sort_width(int n);
 int64_t latent_proj_floats(const pnr_scene &, const pnr_mlp_desc &);
 int launch_latent_proj(const pnr_scene &, const pnr_mlp_weights &, float *, size_t, hipStream_t);
 
 static thread_local char g_err[1024];
+// pnr_render_set_fused: the fused ray march (2, the default: draws + composite in the MLP passes,
+// the fine draws in their own kernel; 1: those too in the coarse epilogue) or the separate
+// sample / composite kernels (0)
+static std::atomic<int> g_fused_march{2};
 
 void set_error(const char *fmt, ...) {
     va_list ap;
@@ -373,33 +379,85 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
         return e == hipSuccess ? PNR_OK : fail(PNR_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(e));
     };
 
-    // coarse pass (nerf.py:273-276)
-    if ((rc = mark(0))) return rc;
-    if ((rc = launch_sample_coarse(rays->rays, n, kc, r_uc, cfg->lindisp, zc, st))) return rc;
-    if ((rc = mark(1))) return rc;
-    if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj,
-                               nullptr, nullptr, 1, n * kc, rawc, xsum, st, nullptr, coarse_proj)))
-        return rc;
-    if ((rc = mark(2))) return rc;
-    if ((rc = launch_composite(zc, rawc, rays->rays, n, kc, cfg->white_bkgd, wc, out->coarse_rgb,
-                               out->coarse_depth, st)))
-        return rc;
-    if ((rc = mark(3))) return rc;
-    if (kf == 0) return PNR_OK;
-    // fine pass (nerf.py:284-301)
+    // Fused ray march (default): each pass is ONE k_point_mlp launch whose prologue draws the
+    // coarse depths and whose epilogue composites the ray from LDS (raw never reaches HBM); the
+    // coarse epilogue also draws the fine samples.  Needs rays that are whole 64-point tiles
+    // (K = 64 or 128); other shapes, and the coarse-output reuse below, take the separate
+    // sample / composite kernels, which run the same device code (march_dev.h).
     const int kall = kc + kf;
-    float *zf = out->z_fine ? out->z_fine : reinterpret_cast<float *>(ws + w.z_f);
-    float *rawf = reinterpret_cast<float *>(ws + w.raw_f);
     // mlp_fine is None (the coarse pack passed twice, models.py:242-255; eval_approx.py --coarse):
     // the kc coarse samples re-enter the fine pass with the MLP that already evaluated them, so
     // only the kf new samples run through it and the coarse outputs are merged in.
-    const bool reuse = fine_packed == coarse_packed && fine_proj == coarse_proj;
+    const bool reuse = kf > 0 && fine_packed == coarse_packed && fine_proj == coarse_proj;
+    const bool fused = g_fused_march.load(std::memory_order_relaxed) != 0;
+    const bool fuse_c = fused && kc % 64 == 0 && kc <= 128;
+    const bool fuse_s = fuse_c && g_fused_march.load(std::memory_order_relaxed) == 1 && kf > 0 && !reuse &&
+                        kc <= 64 && sort_width(kall) <= 128;
+    const bool fuse_f = fused && kf > 0 && !reuse && kall % 64 == 0 && kall <= 128;
+    float *zf = kf > 0 ? (out->z_fine ? out->z_fine : reinterpret_cast<float *>(ws + w.z_f)) : nullptr;
+
+    // coarse pass (nerf.py:273-276)
+    if ((rc = mark(0))) return rc;
+    if (fuse_c) {
+        MarchCfg m = {};
+        m.kpt = kc / 64;
+        m.sample_coarse = 1;
+        m.lindisp = cfg->lindisp;
+        m.white_bkgd = cfg->white_bkgd;
+        m.u_coarse = r_uc;
+        m.z_out = fuse_s ? out->z_coarse : zc;
+        m.weights = fuse_s ? out->coarse_weights : wc;
+        m.rgb = out->coarse_rgb;
+        m.depth = out->coarse_depth;
+        if (fuse_s) {
+            m.kf = kf;
+            m.kfd = kfd;
+            m.n_sort = sort_width(kall);
+            m.depth_std = cfg->depth_std;
+            m.u_fine = r_uf;
+            m.u_jit = r_uj;
+            m.n_depth = r_nd;
+            m.z_fine = zf;
+        }
+        if ((rc = mark(1))) return rc;
+        if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj, nullptr,
+                                   nullptr, 1, n * kc, reuse ? rawc : nullptr, xsum, st, nullptr, coarse_proj, &m)))
+            return rc;
+        if ((rc = mark(2))) return rc;
+    } else {
+        if ((rc = launch_sample_coarse(rays->rays, n, kc, r_uc, cfg->lindisp, zc, st))) return rc;
+        if ((rc = mark(1))) return rc;
+        if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj,
+                                   nullptr, nullptr, 1, n * kc, rawc, xsum, st, nullptr, coarse_proj)))
+            return rc;
+        if ((rc = mark(2))) return rc;
+        if ((rc = launch_composite(zc, rawc, rays->rays, n, kc, cfg->white_bkgd, wc, out->coarse_rgb,
+                                   out->coarse_depth, st)))
+            return rc;
+    }
+    if ((rc = mark(3))) return rc;
+    if (kf == 0) return PNR_OK;
+    // fine pass (nerf.py:284-301)
+    float *rawf = reinterpret_cast<float *>(ws + w.raw_f);
     int *origin = reuse ? reinterpret_cast<int *>(ws + w.origin) : nullptr;
     float *z_new = reuse ? reinterpret_cast<float *>(ws + w.z_new) : nullptr;
-    if ((rc = launch_sample_fine(rays->rays, n, kc, zc, wc, out->coarse_depth, kf, kfd, cfg->depth_std,
-                                 r_uf, r_uj, r_nd, cfg->lindisp, zf, st, origin, z_new)))
+    if (!fuse_s && (rc = launch_sample_fine(rays->rays, n, kc, zc, wc, out->coarse_depth, kf, kfd, cfg->depth_std,
+                                            r_uf, r_uj, r_nd, cfg->lindisp, zf, st, origin, z_new)))
         return rc;
     if ((rc = mark(4))) return rc;
+    if (fuse_f) {
+        MarchCfg m = {};
+        m.kpt = kall / 64;
+        m.white_bkgd = cfg->white_bkgd;
+        m.weights = out->fine_weights;
+        m.rgb = out->fine_rgb;
+        m.depth = out->fine_depth;
+        if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, zf, kall, rays->rays_per_obj, nullptr,
+                                   nullptr, 1, n * kall, nullptr, xsum, st, nullptr, fine_proj, &m)))
+            return rc;
+        if ((rc = mark(5))) return rc;
+        return mark(6);
+    }
     if (reuse) {
         float *raw_new = reinterpret_cast<float *>(ws + w.raw_new);
         if ((rc = launch_point_mlp(*scene, *desc, fine_packed, rays->rays, z_new, kf, rays->rays_per_obj,
@@ -416,6 +474,8 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
         return rc;
     return mark(6);
 }
+
+int32_t pnr_render_set_fused(int32_t on) { return g_fused_march.exchange(on < 0 || on > 2 ? 2 : on); }
 
 int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse, const float *u_coarse,
                       int32_t lindisp, float *z, pnr_stream_t stream) {

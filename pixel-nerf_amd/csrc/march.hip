@@ -6,37 +6,24 @@
 // so every cross-sample step is a wave64 shuffle scan or an LDS sort private
 // to that wave.  Loads of the (B, K) / (B, K, 4) tensors are coalesced:
 // lane k of chunk c reads sample c*64+k.
-#include "pnr_common.h"
+#include "march_dev.h"
 
 namespace pnr {
 
 // ---------------------------------------------------------------------------
-// sample_coarse — nerf.py:98-118
-//   t_k = linspace(0, 1 - 1/Kc, Kc)[k] + u_k / Kc ;  z = near (1 - t) + far t
-// torch.linspace evaluates the first half as start + step*i and the second half
-// as end - step*(steps-1-i) (ATen RangeFactoriesKernel); we follow that form.
+// sample_coarse — nerf.py:98-118 (coarse_z, march_dev.h)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float linspace_at(int i, int n, float end, float step) {
-    if (n == 1) return 0.0f;
-    return (i < n / 2) ? mul_rn(step, (float)i) : sub_rn(end, mul_rn(step, (float)(n - 1 - i)));
-}
-
 __global__ void k_sample_coarse(const float *__restrict__ rays, int64_t n_rays, int kc,
                                 const RngSrc u, int lindisp, float *__restrict__ z) {
     const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n_rays * kc) return;
     const int64_t b = idx / kc;
     const int k = (int)(idx - b * kc);
-    const float near = rays[b * 8 + 6], far = rays[b * 8 + 7];
-    const float end = (float)(1.0 - 1.0 / (double)kc);
-    const float lstep = (kc > 1) ? __fdiv_rn(end, (float)(kc - 1)) : 0.0f;
-    const float step = (float)(1.0 / (double)kc);
-    float t = add_rn(linspace_at(k, kc, end, lstep), mul_rn(rng_uniform(u, b, kc, k), step));
-    z[idx] = t_to_z(t, near, far, lindisp != 0);
+    z[idx] = coarse_z(u, b, kc, k, rays[b * 8 + 6], rays[b * 8 + 7], lindisp != 0);
 }
 
 // ---------------------------------------------------------------------------
-// sample_fine + sample_fine_depth + sort — nerf.py:120-161, 284-295
+// sample_fine + sample_fine_depth + sort — nerf.py:120-161, 284-295 (sample_fine_wave)
 // One 64-lane block per ray.  LDS: cdf[Kc+1] then the sort buffer[N].
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(64) void k_sample_fine(
@@ -51,78 +38,9 @@ __global__ __launch_bounds__(64) void k_sample_fine(
     int *si = reinterpret_cast<int *>(s + n_sort);   // origin of each sorted value (origin != NULL)
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
-    const float near = rays[b * 8 + 6], far = rays[b * 8 + 7];
-    const float *w = weights + b * kc;
-
-    // pdf = (w + 1e-5) / sum(w + 1e-5)   (nerf.py:130-131)
-    float part = 0.0f;
-    for (int k = lane; k < kc; k += 64) part += add_rn(w[k], 1e-5f);
-    const float total = wave_sum(part);
-    // cdf = [0, cumsum(pdf)]; torch's CPU cumsum accumulates in double (acc_type),
-    // rounding every prefix to fp32 — a double wave scan reproduces those values.
-    double carry = 0.0;
-    if (lane == 0) cdf[0] = 0.0f;
-    for (int c0 = 0; c0 < kc; c0 += 64) {
-        const int k = c0 + lane;
-        double p = (k < kc) ? (double)__fdiv_rn(add_rn(w[k], 1e-5f), total) : 0.0;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            double q = __shfl_up(p, off, 64);
-            if (lane >= off) p += q;
-        }
-        if (k < kc) cdf[k + 1] = (float)(carry + p);
-        carry += __shfl(p, 63, 64);
-    }
-    __syncthreads();
-
-    const int nf = kf - kfd;
-    const float inv_steps = (float)kc;
-    // importance samples (nerf.py:135-148)
-    for (int j = lane; j < nf; j += 64) {
-        const float u = rng_uniform(u_fine, b, nf, j);
-        // searchsorted(cdf, u, right=True): number of cdf entries <= u
-        int lo = 0, hi = kc + 1;
-        while (lo < hi) {
-            int mid = (lo + hi) >> 1;
-            if (cdf[mid] <= u) lo = mid + 1; else hi = mid;
-        }
-        float ind = fmaxf(sub_rn((float)lo, 1.0f), 0.0f);
-        float t = __fdiv_rn(add_rn(ind, rng_uniform(u_jit, b, nf, j)), inv_steps);
-        s[kc + j] = t_to_z(t, near, far, lindisp != 0);
-    }
-    // depth samples (nerf.py:157-160): clamp(depth + N(0,1) * std, near, far)
-    for (int j = lane; j < kfd; j += 64) {
-        float zz = add_rn(depth[b], mul_rn(rng_normal(n_depth, b, kfd, j), depth_std));
-        s[kc + nf + j] = fmaxf(fminf(zz, far), near);
-    }
-    for (int k = lane; k < kc; k += 64) s[k] = z_coarse[b * kc + k];
-    for (int k = kc + kf + lane; k < n_sort; k += 64) s[k] = __builtin_inff();
-    __syncthreads();
-    if (origin) {   // the new samples in draw order, and every value's index in cat(coarse, new)
-        for (int j = lane; j < kf; j += 64) z_new[b * kf + j] = s[kc + j];
-        for (int k = lane; k < n_sort; k += 64) si[k] = k;
-        __syncthreads();
-    }
-    // bitonic sort of n_sort values, ascending (torch.sort, nerf.py:295)
-    for (int size = 2; size <= n_sort; size <<= 1) {
-        for (int j = size >> 1; j > 0; j >>= 1) {
-            for (int t = lane; t < (n_sort >> 1); t += 64) {
-                const int lo = 2 * j * (t / j) + (t % j);
-                const int hi = lo + j;
-                const bool asc = (lo & size) == 0;
-                float a = s[lo], c = s[hi];
-                if ((a > c) == asc) {
-                    s[lo] = c; s[hi] = a;
-                    if (origin) { const int t0 = si[lo]; si[lo] = si[hi]; si[hi] = t0; }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    const int k_all = kc + kf;
-    for (int k = lane; k < k_all; k += 64) z_fine[b * k_all + k] = s[k];
-    if (origin)
-        for (int k = lane; k < k_all; k += 64) origin[b * k_all + k] = si[k];
+    sample_fine_wave(lane, b, rays[b * 8 + 6], rays[b * 8 + 7], kc, weights + b * kc, z_coarse + b * kc,
+                     kfd > 0 ? depth[b] : 0.f, kf, kfd, depth_std, u_fine, u_jit, n_depth, lindisp != 0, n_sort,
+                     cdf, s, si, z_fine, origin, z_new);
 }
 
 // raw_f[b][k] = raw of sorted fine sample k: the coarse pass's output for a coarse sample
@@ -141,7 +59,7 @@ __global__ __launch_bounds__(256) void k_merge_raw(const int *__restrict__ origi
 }
 
 // ---------------------------------------------------------------------------
-// composite — nerf.py:176-249
+// composite — nerf.py:176-249 (composite_wave, march_dev.h)
 //   delta_i = z_{i+1} - z_i, delta_last = far - z_last
 //   alpha = 1 - exp(-delta * relu(sigma));  T = excl. cumprod(1 - alpha + 1e-10)
 //   w = alpha * T;  rgb = sum w c;  depth = sum w z;  white: rgb += 1 - sum w
@@ -172,60 +90,8 @@ __global__ __launch_bounds__(256) void k_composite_s(
         zk[i] = __builtin_nontemporal_load(zr + kc);
         v[i] = __builtin_nontemporal_load(rr + kc);
     }
-    const float z_next_lane = dpp_f<0x130>(far, zk[0]);   // wave_shl:1 (lane + 1)
-    float alpha[S];
-    double lp[S + 1];   // exclusive in-lane prefix products
-    lp[0] = 1.0;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const int k = k0 + i;
-        const bool valid = k < K;
-        const float zn = k + 1 >= K ? far : (i + 1 < S ? zk[i + 1] : z_next_lane);
-        const float delta = sub_rn(zn, zk[i]);
-        alpha[i] = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v[i].w, 0.0f)))) : 0.0f;
-        const float shifted = valid ? add_rn(sub_rn(1.0f, alpha[i]), 1e-10f) : 1.0f;
-        lp[i + 1] = lp[i] * (double)shifted;
-    }
-    const double excl = wave_shr1(wave_scan_mul(lp[S]), 1.0);   // product of earlier lanes
-    float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
     float wk[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const bool valid = k0 + i < K;
-        wk[i] = valid ? mul_rn(alpha[i], (float)(excl * lp[i])) : 0.f;
-        sr += mul_rn(wk[i], v[i].x);
-        sg += mul_rn(wk[i], v[i].y);
-        sb += mul_rn(wk[i], v[i].z);
-        sd += mul_rn(wk[i], zk[i]);
-        sw += wk[i];
-    }
-    if (weights) {
-        float *wp = weights + b * K + k0;
-        if (S == 2 && (K & 1) == 0 && k0 < K) {   // 8-B aligned pair
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            __builtin_nontemporal_store(f2{wk[0], wk[1]}, reinterpret_cast<f2 *>(wp));
-        } else {
-#pragma unroll
-            for (int i = 0; i < S; ++i)
-                if (k0 + i < K) __builtin_nontemporal_store(wk[i], wp + i);
-        }
-    }
-    sr = wave_sum_dpp(sr);
-    sg = wave_sum_dpp(sg);
-    sb = wave_sum_dpp(sb);
-    sd = wave_sum_dpp(sd);
-    sw = wave_sum_dpp(sw);
-    if (lane == 0) {
-        if (white_bkgd) {
-            sr = sub_rn(add_rn(sr, 1.0f), sw);
-            sg = sub_rn(add_rn(sg, 1.0f), sw);
-            sb = sub_rn(add_rn(sb, 1.0f), sw);
-        }
-        rgb_out[b * 3 + 0] = sr;
-        rgb_out[b * 3 + 1] = sg;
-        rgb_out[b * 3 + 2] = sb;
-        depth_out[b] = sd;
-    }
+    composite_wave<S>(lane, b, K, far, zk, v, white_bkgd, weights, rgb_out, depth_out, wk);
 }
 
 // any K: 64-sample chunks, one wave scan per chunk with a running carry

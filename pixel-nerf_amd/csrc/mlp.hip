@@ -19,7 +19,19 @@
 //     every wave streams its own 8 row tiles with 16-byte coalesced loads straight
 //     into VGPRs, one k-block (16 k) ahead of the MFMAs.  x (the residual stream)
 //     and h stay in accumulator registers for the whole network.
-#include "pnr_common.h"
+#ifdef PNR_EPI_TIMING   // diagnostic: wave cycles of the fused epilogue's parts (pnr_debug_epi)
+__device__ unsigned long long g_epi[8];
+#define EPI_DECL uint64_t epi_last_ = __builtin_amdgcn_s_memtime();
+#define EPI_T(i)                                                                  \
+    do {                                                                          \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();                         \
+        if (lane == 0) atomicAdd(&g_epi[i], (unsigned long long)(t_ - epi_last_)); \
+        epi_last_ = t_;                                                           \
+    } while (0)
+#endif
+#include <cstddef>
+
+#include "march_dev.h"
 
 namespace pnr {
 namespace mlpk {
@@ -320,6 +332,11 @@ struct Args {
     int64_t proj_stride;
     // dynamic tile scheduling: 8 per-XCD tile counters, 64 B apart (zeroed per launch)
     int *tile_ctr;
+    // fused ray march (render mode, K = 64 m.kpt): a workgroup takes a ray's kpt tiles in a
+    // row, keeps their z and head outputs in LDS and composites the ray in the epilogue of
+    // its last tile (march_epilogue); `out` may then be NULL (raw never reaches HBM)
+    int march;
+    MarchCfg m;
 };
 
 // floats of the activation save per point (Args::save): the fp32 regions, then the relu
@@ -1066,8 +1083,73 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
     PT(g, 2);
 }
 
-// PZ: lin_z from the projected latent (gather_proj) instead of the latent gather + GEMM
-template <int PREC, bool PZ>
+// The march config read where it is used (kernarg s_loads through a pointer the compiler cannot
+// see through): hoisted out of the tile loop, its ~30 loop-invariant dwords held SGPRs across
+// the GEMMs and spilled them (256 SGPR spills, 40 B/lane of VGPR scratch against 16).
+typedef const __attribute__((address_space(4))) MarchCfg *CfgPtr;
+// (k_point_mlp's only parameter is Args, so Args::m sits at offsetof(Args, m) in the kernarg
+// segment; taking &a instead would copy the whole by-value Args to the stack)
+__device__ __forceinline__ CfgPtr march_cfg(const Args &) {
+    uint64_t v = (uint64_t)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() +
+                            offsetof(Args, m));
+    asm volatile("" : "+s"(v));
+    return (CfgPtr)v;
+}
+__device__ __forceinline__ RngSrc ld_rng(const __attribute__((address_space(4))) RngSrc &r) {
+    RngSrc o;
+    o.p = r.p;
+    o.seed = r.seed;
+    o.offset = r.offset;
+    o.stream = r.stream;
+    return o;
+}
+// Fused ray march, one wave: composite ray b from the z / head outputs its kpt tiles left in
+// LDS (buf: z [128] | raw [128][4]; nf: near, far) with the standalone composite's code
+// (composite_wave), then, in a coarse pass that feeds a fine pass, draw the ray's fine
+// samples (sample_fine_wave) from the weights it just computed (scr: w | cdf | sort).  The
+// Philox draws come first: they depend only on the ray, so their latency overlaps the
+// composite's.
+template <int S>
+__device__ __forceinline__ void march_ray(const Args &a, int64_t b, const float *buf, const float *nf, float *scr,
+                                          int lane) {
+    const CfgPtr c = march_cfg(a);
+    EPI_DECL
+    const int kf = c->kf;
+    FineDraws d = {0.f, 0.f, 0.f};
+    if (kf > 0) d = fine_draws(lane, b, kf, c->kfd, ld_rng(c->u_fine), ld_rng(c->u_jit), ld_rng(c->n_depth));
+    const float near = nf[0], far = nf[1];
+    float zk[S], wk[S];
+    f4 v[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        zk[i] = buf[S * lane + i];
+        v[i] = *reinterpret_cast<const f4 *>(buf + 128 + 4 * (S * lane + i));
+    }
+    const float depth = composite_wave<S>(lane, b, a.K, far, zk, v, c->white_bkgd, c->weights, c->rgb, c->depth, wk);
+    EPI_T(0);
+#ifdef PNR_EPI_TIMING
+    if (lane == 0) atomicAdd(&g_epi[7], 1ull);
+#endif
+    if (kf > 0) {
+        float *w = scr;
+#pragma unroll
+        for (int i = 0; i < S; ++i) w[S * lane + i] = wk[i];
+        wave_lds_sync();
+        sample_fine_wave(lane, b, near, far, a.K, w, buf, depth, kf, c->kfd, c->depth_std, RngSrc{}, RngSrc{},
+                         RngSrc{}, c->lindisp != 0, c->n_sort, scr + 128, scr + 256, nullptr, c->z_fine, nullptr,
+                         nullptr, true, d);
+    }
+}
+__device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const float *buf, const float *nf,
+                                               float *scr, int lane) {
+    if (march_cfg(a)->kpt == 1) march_ray<1>(a, b, buf, nf, scr, lane);
+    else march_ray<2>(a, b, buf, nf, scr, lane);
+}
+
+// PZ: lin_z from the projected latent (gather_proj) instead of the latent gather + GEMM;
+// MARCH: the fused ray march (a.m), a separate instantiation so that the plain point model
+// keeps its own register allocation
+template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     constexpr int KD = PZ ? H_DIST : H_DIST_3;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1174,17 +1256,25 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // the launch.  The next tile is fetched before the head, so the atomic's latency hides.
     int *s_next = reinterpret_cast<int *>(petab + 32);
     float *hpart = petab + 64;   // PREC 3 head: k-half partials [wave][lane][4] (8 KB)
+    // fused march (MARCH): the ray's z [128] | head outputs [128][4], the epilogue scratch,
+    // near / far.  (Deferring a ray's epilogue into the next tile, under the SIMD-mate's MFMAs,
+    // was measured: the double buffers and the call inside the GEMM region cost more in spills
+    // than it hid.)
+    float *mreg = PREC == 3 ? hpart + 2048 : petab + 36;
+    float *mscr = mreg + MARCH_BUF_FLOATS;
+    float *mnf = mscr + 384;
+    const int kpt = MARCH ? march_cfg(a)->kpt : 1;   // tiles per scheduling unit (a ray when marching)
     auto grab = [&]() -> int {
-        const int64_t T = a.n_tiles;
+        const int64_t T = a.n_tiles >> (kpt - 1);   // kpt is 1 or 2
         const int x0 = blockIdx.x & 7;
         for (int k = 0; k < 8; ++k) {
             const int x = (x0 + k) & 7;
             const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
             if (lo >= hi) continue;
             const int64_t i = lo + atomicAdd(a.tile_ctr + 16 * x, 1);
-            if (i < hi) return (int)i;
+            if (i < hi) return (int)(i << (kpt - 1));
         }
-        return (int)T;
+        return (int)a.n_tiles;
     };
     if (tid == 0) *s_next = grab();
     lds_barrier();
@@ -1202,12 +1292,20 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             const int64_t p = p_raw < a.n_points ? p_raw : a.n_points - 1;
             // the point (re-read per view from L2 rather than held in registers across the
             // per-view blocks' GEMMs)
-            float px, py, pz, dx, dy, dz;
+            float px, py, pz, dx, dy, dz, zz = 0.f;
             int64_t obj;
             if (a.render_mode) {
                 const int64_t b = p / a.K;
                 const float *ray = a.rays + b * 8;
-                const float zz = a.zs[p];
+                // the coarse draw in the prologue (nerf.py:98-118), or the given depth
+                if (MARCH && march_cfg(a)->sample_coarse) {
+                    const CfgPtr m = march_cfg(a);
+                    zz = coarse_z(ld_rng(m->u_coarse), b, a.K, (int)(p - b * a.K), ray[6], ray[7], m->lindisp != 0);
+                    float *zo = m->z_out;
+                    if (zo && qt == 0 && v == 0) zo[p] = zz;
+                } else {
+                    zz = a.zs[p];
+                }
                 dx = ray[3]; dy = ray[4]; dz = ray[5];
                 // points = o + z * d  (nerf.py:185)
                 px = add_rn(ray[0], mul_rn(zz, dx));
@@ -1238,6 +1336,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             // features f = FPT qt .. FPT qt + FPT - 1 of [xyz_rot | PE | viewdir_cam | 0]
             lds_barrier();   // previous users of inbuf are done
             PT(gc, 10);
+            if (MARCH && qt == 0 && v == 0) {   // for the epilogue
+                mreg[(int)(tile & (kpt - 1)) * COLS + col] = zz;
+                if (col == 0 && (tile & (kpt - 1)) == 0) {
+                    const float *rr = a.rays + (tile >> (kpt - 1)) * 8;
+                    mnf[0] = rr[6];
+                    mnf[1] = rr[7];
+                }
+            }
             {
                 const int npe = 3 * L.pe_n;
                 float fv[FPT];
@@ -1485,7 +1591,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                       PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
-        if (tid == 0) *s_next = grab();   // read after the barrier closing this iteration
+        if (tid == 0) *s_next = (tile + 1) & (kpt - 1) ? tile + 1 : grab();   // read after the closing barrier
         pre_publish_sync();
         publish_relu(x, tile, 2 * L.n_blocks, 0);
         lds_barrier();
@@ -1542,7 +1648,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
                 r.w = fmaxf(o.w, 0.f);
-                *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+                if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+                if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * ((int)(tile & (kpt - 1)) * COLS + 16 * wave + cl)) = r;
             }
         }
         PT(gc, 4);
@@ -1562,8 +1669,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
                 r.w = fmaxf(o.w, 0.f);
-                *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+                if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+                if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * ((int)(tile & (kpt - 1)) * COLS + 16 * wave + cc)) = r;
             }
+        }
+        // ---- fused march: the ray's last tile composites it (and draws its fine samples) --
+        if (MARCH && ((tile + 1) & (kpt - 1)) == 0) {   // kpt is 1 or 2
+            lds_barrier();   // the ray's head outputs visible
+            if (wave == WAVES - 1) march_epilogue(a, tile >> (kpt - 1), mreg, mnf, mscr, opaque_lane(lane));
         }
     }
 #ifdef PNR_PHASE_TIMING
@@ -1823,6 +1936,13 @@ k_bias_reduce(const float *__restrict__ part, int n_wg, int n, float *__restrict
 // ------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------
+#ifdef PNR_EPI_TIMING
+extern "C" int pnr_debug_epi(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(::g_epi), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    static const unsigned long long zero[8] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(::g_epi), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef PNR_PHASE_TIMING
 // diagnostic: copy (and optionally clear) the phase counters; not part of the ABI
 extern "C" int pnr_debug_phase(unsigned long long *out, int reset) {
@@ -1999,9 +2119,12 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
                      const float *rays, const float *zs, int K, int64_t rays_per_obj,
                      const float *xyz, const float *dirs, int64_t points_per_obj,
                      int64_t n_points, float *out, float *xsum_ws, hipStream_t st, float *save,
-                     const float *proj) {
+                     const float *proj, const MarchCfg *march) {
     if (n_points == 0) return PNR_OK;
     if (proj && save) return fail(PNR_ERR_UNSUPPORTED, "the activation save (training) needs the latent gather path");
+    if (march && (!rays || save || (march->kpt != 1 && march->kpt != 2) || K != mlpk::COLS * march->kpt ||
+                  n_points % K != 0 || (march->kf > 0 && (K > 64 || march->n_sort > 128 || K + march->kf > march->n_sort))))
+        return fail(PNR_ERR_INVALID, "point_mlp: fused march needs K = 64 kpt (kpt 1 or 2) and kc + kf <= 128");
     mlpk::Args a = {};
     a.packed = static_cast<const float *>(packed);
     a.L = mlpk::make_layout(d);
@@ -2014,6 +2137,8 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     a.img_w = sc.image_w; a.img_h = sc.image_h;
     a.out = out;
     a.xsum = xsum_ws;
+    a.march = march != nullptr;
+    if (march) a.m = *march;
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
     a.save = save;
     a.proj = proj;
@@ -2026,13 +2151,16 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     // PREC 3: split image P0 + P1, gather records, column maxima, exponents, PE table, next tile
     //         = 143,760 B; else: fp32 activations + staging ring + gather records + PE table +
     //         next tile = 158,864 B
-    const size_t lds = d.precision == PNR_PREC_F16X3
+    const size_t lds = (d.precision == PNR_PREC_F16X3
         ? 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (2 * mlpk::COLS * 8 + mlpk::COLS + 64 + 2048)
-        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8 + 32 + 4);
+        : sizeof(float) * ((size_t)mlpk::COLS * mlpk::LDS_LD + 2 * mlpk::STG_FLOATS + mlpk::COLS * 8 + 32 + 4)
+        ) + (march ? sizeof(float) * MARCH_LDS_FLOATS : 0);   // + the fused march region
 #define PNR_LAUNCH_MLP(P)                                                                              \
     do {                                                                                               \
-        if (proj) hipLaunchKernelGGL((mlpk::k_point_mlp<P, true>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \
-        else hipLaunchKernelGGL((mlpk::k_point_mlp<P, false>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);     \
+        if (proj && march) hipLaunchKernelGGL((mlpk::k_point_mlp<P, true, true>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \
+        else if (proj) hipLaunchKernelGGL((mlpk::k_point_mlp<P, true, false>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \
+        else if (march) hipLaunchKernelGGL((mlpk::k_point_mlp<P, false, true>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a); \
+        else hipLaunchKernelGGL((mlpk::k_point_mlp<P, false, false>), dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);     \
     } while (0)
     switch (d.precision) {
     case PNR_PREC_F16X3: PNR_LAUNCH_MLP(3); break;

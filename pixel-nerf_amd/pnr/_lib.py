@@ -94,6 +94,7 @@ SIGNATURES = {
                                         ctypes.POINTER(Rays), ctypes.POINTER(Rng),
                                         ctypes.POINTER(RenderCfg), ctypes.POINTER(RenderOut),
                                         c_vp, c_size, c_vp, ctypes.POINTER(c_vp)]),
+    "pnr_render_set_fused": (c_i32, [c_i32]),
     "pnr_sample_coarse": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_i32, c_vp, c_vp]),
     "pnr_sample_fine": (c_i32, [c_vp, c_i64, c_i32, c_vp, c_vp, c_vp, c_i32, c_i32, c_f, c_vp,
                                 c_vp, c_vp, c_i32, c_vp, c_vp]),
@@ -139,6 +140,8 @@ def load():
                        "__graft_entry__.build()" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
+        if os.environ.get("PNR_LIB_PATH") and not hasattr(lib, name):
+            continue   # an older diagnostic build (A/B against a previous revision)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -160,6 +163,23 @@ def ptr(t):
     if t is None:
         return None
     return ctypes.c_void_p(t.data_ptr())
+
+
+class fused_march:
+    """Context manager: pnr_render_set_fused(mode) inside, the previous setting restored after
+    (2, the default: fused passes + fine-draw kernel; 1: fine draws in the coarse epilogue too;
+    0: the separate sample / composite kernels)."""
+
+    def __init__(self, mode):
+        self.on = int(mode)
+
+    def __enter__(self):
+        self.prev = load().pnr_render_set_fused(self.on)
+        return self
+
+    def __exit__(self, *exc):
+        load().pnr_render_set_fused(self.prev)
+        return False
 
 
 def stream_of(device):

@@ -9,7 +9,7 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/pixel-nerf_amd/build/$tag
 src=$out/src
 rm -rf "$out"; mkdir -p "$src/csrc" "$src/include"
-for f in march.hip mlp.hip train.hip encoder.hip wgrad.hip proj.hip abi.cpp pnr_common.h; do
+for f in march.hip mlp.hip train.hip encoder.hip wgrad.hip proj.hip abi.cpp pnr_common.h march_dev.h; do
   if [ "$rev" = WORKTREE ]; then cp "$root/pixel-nerf_amd/csrc/$f" "$src/csrc/$f"
   else git -C "$root" show "$rev:pixel-nerf_amd/csrc/$f" > "$src/csrc/$f" 2>/dev/null || rm -f "$src/csrc/$f"; fi
 done

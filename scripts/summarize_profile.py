@@ -25,6 +25,15 @@ def read_counter(path):
     return rows
 
 
+def pass_of(name, last):
+    """Render pass of a k_point_mlp launch: the sampler launched before it names it; the fused
+    march instantiation (k_point_mlp<P, Z, true>) draws its coarse depths itself, so one with
+    no sampler before it is a coarse pass (pnr_render_set_fused mode 2)."""
+    if last == "query" and name.replace(" ", "").endswith(",true>"):
+        return "coarse"
+    return last
+
+
 def kname(full):
     """'void pnr::mlpk::k_point_mlp<3>(pnr::mlpk::Args)' -> 'pnr::mlpk::k_point_mlp<3>'"""
     n = full.split("(")[0].strip()
@@ -55,7 +64,7 @@ def main():
             last = "fine"
         elif "k_point_mlp" in name:
             ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
-            rows.append((name, last, ms))
+            rows.append((name, pass_of(name, last), ms))
             last = "query"
     stats = ["kernel,pass,launches,avg_ms,min_ms,max_ms"]
     for key in sorted(set((n, p) for n, p, _ in rows)):
@@ -82,7 +91,7 @@ def main():
             last = "fine"
         label = ""
         if "k_point_mlp" in name:
-            label, last = last, "query"
+            label, last = pass_of(name, last), "query"
         fk = float(r["Counter_Value"])
         wk = wmap.get(r["Dispatch_Id"], 0.0)
         ms = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6

@@ -721,3 +721,66 @@ def test_torch_ops_render_rays_matches_fixture(name):
     # composite: the operator on the fine samples and the fused march's fine weights agree
     w, rgb, depth = ops_.composite(z_f, torch.rand(B, z_f.shape[-1], 4, device=DEV), rays, True, True)
     assert w.shape == z_f.shape and rgb.shape == (B, 3) and depth.shape == (B,)
+
+
+# ------------------------------------------------------------- fused ray march --
+@pytest.mark.parametrize("precision", PRECS)
+@pytest.mark.parametrize("kc,kf,kfd,white,lindisp,n_views,sb", [
+    (64, 64, 0, True, False, 1, 1),      # cfg2 / cfg3: both passes fused, fine draws in the coarse epilogue
+    (64, 32, 16, True, False, 1, 1),     # shipped conf: coarse fused (+ fine draws), fine pass K = 96 separate
+    (64, 0, 0, False, True, 1, 1),       # coarse only
+    (128, 0, 0, True, False, 1, 1),      # two tiles per ray
+    (32, 32, 0, True, False, 1, 1),      # coarse K = 32 separate, fine K = 64 fused
+    (64, 64, 16, False, False, 3, 2),    # multi-view mean, two objects, depth samples
+])
+def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_views, sb):
+    """The fused ray march (pnr_render_set_fused: mode 2, the default, sampling + MLP + composite
+    in k_point_mlp with the fine draws in their own kernel; mode 1, the fine draws in the coarse
+    epilogue too) is bit-identical to the separate sample / MLP / composite kernels (mode 0) for
+    every output, in every arithmetic; the fixture tests above hold the default path to the
+    oracle."""
+    from pnr import _lib
+
+    from pnr import util
+
+    n_rays = 1024
+    sd = synth.pixelnerf_state(1)
+    if n_views == 1 and sb == 1:
+        sc = synth.scene_srn(seed=5, n_rays=n_rays, pick="all")
+        lat, poses, focal, wh, c, rays = sc["latent"], sc["poses"], sc["focal"], (128, 128), None, sc["rays"]
+    else:
+        lat = synth.latent(10, sb * n_views, 512, 30, 40)
+        poses = synth.srn_poses([30.0 * i for i in range(sb * n_views)], radius=1.4).reshape(sb, n_views, 4, 4)
+        focal, wh, c = torch.tensor(90.0), (96, 80), None
+        rays = util.gen_rays(synth.srn_poses([15.0 + 40.0 * i for i in range(sb)], radius=1.4), 96, 80,
+                             focal, 0.4, 2.4).reshape(sb, -1, 8)
+        idx = torch.from_numpy((synth.hash_uniform(3, n_rays) * rays.shape[1]).astype("int64"))
+        rays = rays[:, idx].contiguous()
+    net = PixelNeRFNet(model_conf())
+    net.mlp_precision = precision
+    net.load_state_dict(sd, strict=False)
+    net = net.to(DEV).eval()
+    net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), wh,
+                      c=None if c is None else c.to(DEV), num_objs=sb)
+    r = NeRFRenderer(n_coarse=kc, n_fine=kf, n_fine_depth=kfd, depth_std=0.01, white_bkgd=white,
+                     lindisp=lindisp)
+    r.return_z = True
+    rays = rays.to(DEV).reshape(sb, -1, 8)
+    outs = []
+    for mode in (0, 1, 2):   # separate kernels, full fusion, fused passes + fine-draw kernel
+        with _lib.fused_march(mode), torch.no_grad():
+            torch.manual_seed(11)
+            outs.append(r(net, rays, want_weights=True))
+    torch.cuda.synchronize()
+    b = outs[0]
+    for mode, a in ((1, outs[1]), (2, outs[2])):
+        for p in (("coarse", "fine") if kf > 0 else ("coarse",)):
+            for k in ("rgb", "depth", "weights", "z"):
+                x, y = getattr(a[p], k, None), getattr(b[p], k, None)
+                if y is None:
+                    continue
+                assert x is not None and torch.equal(x, y), (mode, p, k, float((x - y).abs().max())
+                                                             if x is not None else None)
+    a = outs[2]
+    w = a.coarse.weights
+    assert bool((w >= 0).all()) and float(w.sum(-1).max()) <= 1.0 + 1e-5

@@ -22,6 +22,8 @@ net.encode_latent(synth.latent(0, 1, 512, 64, 64).to(dev), synth.srn_poses([0.0]
                   torch.tensor(131.25, device=dev), (128, 128))
 rays = util.gen_rays(synth.srn_poses([30.0]).to(dev), 128, 128, torch.tensor(131.25), 0.01, 4.0).reshape(-1, 8)
 r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True)
+if hasattr(_lib.load(), "pnr_render_set_fused"):
+    _lib.load().pnr_render_set_fused(int(os.environ.get("PNR_FUSED", "1")))
 dbg = getattr(_lib.load(), "pnr_debug_phase", None)   # PNR_PHASE_TIMING variant only
 ph = (ctypes.c_ulonglong * 32)()
 with torch.no_grad():
@@ -33,7 +35,14 @@ with torch.no_grad():
     for i in range(n):
         r(net, rays[4096 * (i % 4):4096 * (i % 4 + 1)][None])
     torch.cuda.synchronize()
-print("done", prec, n, "chunk_ms %.3f" % ((time.perf_counter() - t0) / n * 1e3), os.environ.get("PNR_LIB_PATH", "default"))
+print("done", prec, "fused", os.environ.get("PNR_FUSED", "1"), n, "chunk_ms %.3f" % ((time.perf_counter() - t0) / n * 1e3), os.environ.get("PNR_LIB_PATH", "default"))
+epi = getattr(_lib.load(), "pnr_debug_epi", None)   # PNR_EPI_TIMING variant only
+if epi is not None:
+    e = (ctypes.c_ulonglong * 8)()
+    epi(e)   # since the warm-up (counts include it)
+    n_r = max(e[7], 1)
+    print("fused epilogue cycles/ray (the epilogue wave):", {nm: round(e[i] / n_r) for i, nm in
+          enumerate(["composite", "cdf", "draws", "sort+store"])}, "rays", e[7])
 if dbg is not None:
     dbg(ph, 0)
     v = list(ph)
