@@ -381,9 +381,8 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
         dist.barrier()
     elapsed = pdist.max_over_ranks(t1 - t0, dev)
     rays_total = sb * per * steps * world
-    arith = (precision + " forward + f16x3 fused input-gradient chain + split-bf16 (x6) weight gradients"
-             if precision == "f16x3" and ns == 1 else
-             precision + " forward + fp32 GEMM input-gradient chain + split-bf16 (x6) weight gradients"
+    arith = (precision + " forward + f16x3 fused input-gradient chain%s + split-bf16 (x6) weight gradients"
+             % (" (NS = %d views)" % ns if ns > 1 else "")
              if precision == "f16x3" else precision + " forward, fp32 GEMM backward")
     return {
         "metric": "training rays/sec (cfg5: encoder + coarse/fine render + backward + grad all-reduce + Adam)",

@@ -364,6 +364,19 @@ int pnr_mlp_backward_bias(const pnr_mlp_desc *desc, const void *packed, const vo
                           float *dy, float *d_zlat, float *d_bias, void *workspace, size_t workspace_bytes,
                           pnr_stream_t stream);
 
+/* pnr_mlp_backward_bias for n_views >= 1 source views per point (resnetfc.py:151-172 with
+ * util.combine_interleaved's mean): `save` from pnr_render_points with n_views views (its
+ * regions have n_views * n_points rows, row v * n_points + p for the blocks before
+ * combine_layer); dy is (2 n_blocks + 1) x (n_views * n_points) x 512, the slots of the blocks
+ * from combine_layer on (and lin_out's input) using their first n_points rows, the others the
+ * view rows; d_zlat is (n_views * n_points, 512); d_bias sums every slot over all its rows.
+ * The blocks after the mean run once per point; dL/d(mean) / n_views then enters the chain of
+ * the blocks before it once per view.  n_views == 1 is pnr_mlp_backward_bias. */
+int pnr_mlp_backward_views(const pnr_mlp_desc *desc, const void *packed, const void *packed_t,
+                           const float *lin_out_w, const float *save, const float *d_o, int64_t n_points,
+                           int32_t n_views, float *dy, float *d_zlat, float *d_bias, void *workspace,
+                           size_t workspace_bytes, pnr_stream_t stream);
+
 /* Workspace bytes of pnr_weight_grad (n_layers in 1..16); 0 if the sizes are invalid. */
 size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points);
 

@@ -29,7 +29,7 @@ int64_t mlp_save_floats(const pnr_mlp_desc &d, int64_t n_points);
 size_t mlp_packed_t_bytes(const pnr_mlp_desc &);
 int mlp_pack_t(const pnr_mlp_weights &, const void *, void *, size_t, hipStream_t);
 int launch_mlp_bwd(const pnr_mlp_desc &, const void *, const void *, const float *, const float *, const float *,
-                   int64_t, float *, float *, hipStream_t, float *, void *, size_t);
+                   int64_t, float *, float *, hipStream_t, float *, void *, size_t, int n_views);
 size_t mlp_bwd_workspace_bytes(const pnr_mlp_desc &, int64_t);
 size_t wgrad_workspace_bytes(int, int64_t);
 int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
@@ -261,7 +261,15 @@ int pnr_mlp_backward_bias(const pnr_mlp_desc *desc, const void *packed, const vo
                           const float *lin_out_w, const float *save, const float *d_o, int64_t n_points, float *dy,
                           float *d_zlat, float *d_bias, void *workspace, size_t workspace_bytes,
                           pnr_stream_t stream) {
-    if (!desc || n_points < 0) return fail(PNR_ERR_INVALID, "pnr_mlp_backward: bad arguments");
+    return pnr_mlp_backward_views(desc, packed, packed_t, lin_out_w, save, d_o, n_points, 1, dy, d_zlat, d_bias,
+                                  workspace, workspace_bytes, stream);
+}
+
+int pnr_mlp_backward_views(const pnr_mlp_desc *desc, const void *packed, const void *packed_t,
+                           const float *lin_out_w, const float *save, const float *d_o, int64_t n_points,
+                           int32_t n_views, float *dy, float *d_zlat, float *d_bias, void *workspace,
+                           size_t workspace_bytes, pnr_stream_t stream) {
+    if (!desc || n_points < 0 || n_views < 1) return fail(PNR_ERR_INVALID, "pnr_mlp_backward: bad arguments");
     if (n_points > 0 && (!packed || !packed_t || !lin_out_w || !save || !d_o || !dy))
         return fail(PNR_ERR_INVALID, "pnr_mlp_backward: NULL argument");
     if (((reinterpret_cast<uintptr_t>(lin_out_w) | reinterpret_cast<uintptr_t>(save) |
@@ -269,7 +277,7 @@ int pnr_mlp_backward_bias(const pnr_mlp_desc *desc, const void *packed, const vo
           reinterpret_cast<uintptr_t>(d_zlat)) & 15) != 0)
         return fail(PNR_ERR_INVALID, "pnr_mlp_backward: buffers must be 16-byte aligned");
     return launch_mlp_bwd(*desc, packed, packed_t, lin_out_w, save, d_o, n_points, dy, d_zlat, (hipStream_t)stream,
-                          d_bias, workspace, workspace_bytes);
+                          d_bias, workspace, workspace_bytes, n_views);
 }
 
 size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points) {

@@ -1695,6 +1695,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 //                       dx = dx + (W_0^T dh) . [x_b > 0]
 //                       b < n_linz:  dY(lin_z b) = dx,  dzlat += W_z^T dx
 //   dY(lin_in) = dx
+// With NS > 1 source views (resnetfc.py:151-172, util.combine_interleaved) the blocks from
+// combine_layer on run once per point; dL/d(view mean) / NS then enters the chain of the blocks
+// before it once per view, on the forward save's view rows v P + p (masks, dY, dzlat).  View 0
+// stores that value as its first dY slot (dY(fc_1, ncomb - 1)); views 1.. reload it from there.
 // The output gradients dY of every layer go to global memory for the weight gradients
 // (dW = dY^T IN over the points) and the bias gradients (column sums).  Slot order, chosen
 // so that those are strided batched GEMMs over the save's slots:
@@ -1706,12 +1710,14 @@ struct BwdArgs {
     const float *w_out;      // lin_out weight (4 x 512, fp32)
     const float *save;       // forward activation save (Args::save)
     const float *d_o;        // (P, 4) gradient of the pre-head output
-    float *dy;               // (2 nb + 1) x P x 512
-    float *dzlat;            // (P, 512) gradient of the sampled latent (n_linz > 0)
+    float *dy;               // (2 nb + 1) x (NS P) x 512; the slots of the blocks from combine_layer
+                             // on use their first P rows
+    float *dzlat;            // (NS P, 512) gradient of the sampled latent (n_linz > 0)
     float *bsum;             // NULL, or [workgroup][2 nb + 1][512] column sums of each dy slot
                              // over the workgroup's tiles (its tiles in order: deterministic)
     Layout L;
     int64_t n_points, n_tiles;
+    int ns;                  // source views per point (the save's view rows)
 };
 
 // sum over the 16 lanes of a DPP row (every lane gets it; lane 0's order is the fixed tree
@@ -1799,7 +1805,9 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     const int g = lane >> 4, cl = lane & 15;
     const Layout &L = a.L;
     const int nb = L.n_blocks;
-    const int64_t P = a.n_points;
+    const int64_t P = a.n_points, PS = P * a.ns;
+    // blocks [nc, nb) run per point, [0, nc) per view (all per point when NS == 1)
+    const int nc = a.ns > 1 ? L.ncomb : 0;
     // LDS: P0 | P1 | cmax | ecol (as the forward's PREC 3 layout, no gather records)
     _Float16 *P0 = reinterpret_cast<_Float16 *>(smem);
     _Float16 *P1 = P0 + PART_HALVES;
@@ -1813,11 +1821,12 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     gc.ecol = ecol;
     gc.wave = wave;
     gc.lane = lane;
-    // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f
-    const uint32_t *msk = reinterpret_cast<const uint32_t *>(a.save + save_mask_offset(nb, P));
-    auto mask_slot = [&](int i) { return msk + P * 16 * i; };
+    // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f; every
+    // region has PS rows (view rows v P + p before combine_layer)
+    const uint32_t *msk = reinterpret_cast<const uint32_t *>(a.save + save_mask_offset(nb, PS));
+    auto mask_slot = [&](int i, int64_t row0) { return msk + PS * 16 * i + row0 * 16; };
     u2m mk[CT];
-    auto dy_slot = [&](int i) { return a.dy + P * H * i; };
+    auto dy_slot = [&](int i, int64_t row0) { return a.dy + PS * H * i + row0 * H; };
     auto bs_slot = [&](int i) -> float * {
         return a.bsum ? a.bsum + ((int64_t)blockIdx.x * (2 * nb + 1) + i) * H : nullptr;
     };
@@ -1838,9 +1847,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     auto layer = [&](int li) { return a.packed_t + (int64_t)li * L.layer_floats; };
 
     Acc x, h;
+    // segments of the chain: NS == 1: blocks nb-1 .. 0; else blocks nb-1 .. nc per point, then
+    // nc-1 .. 0 once per view on its rows v P + p
+    const int n_seg = a.ns == 1 ? 1 : 1 + a.ns;
     for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
+        const bool first_tile = tile == blockIdx.x;
         {   // dx = (d_o W_out) . [x_f > 0]
-            load_mask(mk, mask_slot(2 * nb), tile, P, wave, lane);
+            load_mask(mk, mask_slot(2 * nb, 0), tile, P, wave, lane);
             f4 wo[4][RTW];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -1857,47 +1870,72 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
             }
             relu_mask(x, mk, tile, P, lane);
         }
-        bool published = false;
-        for (int b = nb - 1; b >= 0; --b) {
-            if (!published) publish(x);
-            store_rows(x, dy_slot(nb + 1 + b), tile, P, wave, lane, bs_slot(nb + 1 + b), tile == blockIdx.x);
-            const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
-            zero(h);
-            load_mask(mk, mask_slot(nb + b), tile, P, wave, lane);   // lands during the GEMM
-            layer_gemm<3, NKB, H_DIST_3>(h, layer(l1), gc, 1 + l1);
-            relu_mask(h, mk, tile, P, lane);
-            store_rows(h, dy_slot(b), tile, P, wave, lane, bs_slot(b), tile == blockIdx.x);
-            publish(h);
-            zero(h);
-            load_mask(mk, mask_slot(b), tile, P, wave, lane);
-            layer_gemm<3, NKB, H_DIST_3>(h, layer(l0), gc, 1 + l0);
-            relu_mask(h, mk, tile, P, lane);
+        for (int sgi = 0; sgi < n_seg; ++sgi) {
+            const int v = sgi - 1;   // the view of a per-view segment
+            const int b_hi = sgi == 0 ? nb : nc, b_lo = sgi == 0 ? nc : 0;
+            const int64_t row0 = v > 0 ? (int64_t)v * P : 0;
+            // the first store of the workgroup to the bias partials of these slots
+            const bool first = first_tile && v <= 0;
+            if (v == 0) {   // torch.mean's backward: dL/d(mean) / NS to every view
+                const float inv = (float)a.ns;
 #pragma unroll
-            for (int r = 0; r < RTW; ++r)
+                for (int r = 0; r < RTW; ++r)
 #pragma unroll
-                for (int c = 0; c < CT; ++c) x[r][c] += h[r][c];
-            published = false;
-            if (b < L.n_linz) {
-                publish(x);
-                published = true;
-                const int lz = layer_index(b, 0, L.n_linz);
-                zero(h);
-                layer_gemm<3, NKB, H_DIST_3>(h, layer(lz), gc, 1 + lz);
-                const bool first = b == L.n_linz - 1;
+                    for (int c = 0; c < CT; ++c) x[r][c] = x[r][c] / inv;
+            } else if (v > 0 && nc > 0) {   // the same, as view 0 stored it (this lane's own rows)
+                const float *src = dy_slot(nb + nc, 0);
+                const int ln = opaque_lane(lane), gz = ln >> 4;
 #pragma unroll
                 for (int c = 0; c < CT; ++c) {
-                    const int ln = opaque_lane(lane), gz = ln >> 4;
                     const int64_t p = tile * COLS + 16 * c + (ln & 15);
-                    if (p >= P) continue;
+                    const int64_t pc = p < P ? p : P - 1;
 #pragma unroll
-                    for (int r = 0; r < RTW; ++r) {
-                        f4 *q = reinterpret_cast<f4 *>(a.dzlat + p * H + 16 * (RTW * wave + r) + 4 * gz);
-                        *q = first ? h[r][c] : *q + h[r][c];
+                    for (int r = 0; r < RTW; ++r)
+                        x[r][c] = *reinterpret_cast<const f4 *>(src + pc * H + 16 * (RTW * wave + r) + 4 * gz);
+                }
+            }
+            bool published = false;
+            for (int b = b_hi - 1; b >= b_lo; --b) {
+                if (!published) publish(x);
+                store_rows(x, dy_slot(nb + 1 + b, row0), tile, P, wave, lane, bs_slot(nb + 1 + b), first);
+                const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
+                zero(h);
+                load_mask(mk, mask_slot(nb + b, row0), tile, P, wave, lane);   // lands during the GEMM
+                layer_gemm<3, NKB, H_DIST_3>(h, layer(l1), gc, 1 + l1);
+                relu_mask(h, mk, tile, P, lane);
+                store_rows(h, dy_slot(b, row0), tile, P, wave, lane, bs_slot(b), first);
+                publish(h);
+                zero(h);
+                load_mask(mk, mask_slot(b, row0), tile, P, wave, lane);
+                layer_gemm<3, NKB, H_DIST_3>(h, layer(l0), gc, 1 + l0);
+                relu_mask(h, mk, tile, P, lane);
+#pragma unroll
+                for (int r = 0; r < RTW; ++r)
+#pragma unroll
+                    for (int c = 0; c < CT; ++c) x[r][c] += h[r][c];
+                published = false;
+                if (b < L.n_linz) {
+                    publish(x);
+                    published = true;
+                    const int lz = layer_index(b, 0, L.n_linz);
+                    zero(h);
+                    layer_gemm<3, NKB, H_DIST_3>(h, layer(lz), gc, 1 + lz);
+                    const bool zfirst = b == L.n_linz - 1;
+#pragma unroll
+                    for (int c = 0; c < CT; ++c) {
+                        const int ln = opaque_lane(lane), gz = ln >> 4;
+                        const int64_t p = tile * COLS + 16 * c + (ln & 15);
+                        if (p >= P) continue;
+#pragma unroll
+                        for (int r = 0; r < RTW; ++r) {
+                            f4 *q = reinterpret_cast<f4 *>(a.dzlat + (row0 + p) * H + 16 * (RTW * wave + r) + 4 * gz);
+                            *q = zfirst ? h[r][c] : *q + h[r][c];
+                        }
                     }
                 }
             }
+            if (b_lo == 0) store_rows(x, dy_slot(nb, row0), tile, P, wave, lane, bs_slot(nb), first);
         }
-        store_rows(x, dy_slot(nb), tile, P, wave, lane, bs_slot(nb), tile == blockIdx.x);
     }
 }
 
@@ -2067,7 +2105,7 @@ size_t mlp_bwd_workspace_bytes(const pnr_mlp_desc &d, int64_t n_points) {
 
 int launch_mlp_bwd(const pnr_mlp_desc &d, const void *packed, const void *packed_t, const float *w_out,
                    const float *save, const float *d_o, int64_t n_points, float *dy, float *dzlat, hipStream_t st,
-                   float *d_bias, void *ws, size_t ws_bytes) {
+                   float *d_bias, void *ws, size_t ws_bytes, int n_views) {
     int rc = mlp_check_desc(d);
     if (rc) return rc;
     if (d.precision != PNR_PREC_F16X3)
@@ -2085,6 +2123,8 @@ int launch_mlp_bwd(const pnr_mlp_desc &d, const void *packed, const void *packed
     a.dzlat = dzlat;
     a.n_points = n_points;
     a.n_tiles = (n_points + mlpk::COLS - 1) / mlpk::COLS;
+    if (n_views < 1) return fail(PNR_ERR_INVALID, "mlp backward: n_views < 1");
+    a.ns = n_views;
     const int64_t grid = mlp_bwd_grid(n_points);
     if (d_bias) {
         const size_t need = mlp_bwd_workspace_bytes(d, n_points);

@@ -118,6 +118,8 @@ SIGNATURES = {
     "pnr_mlp_backward_workspace_bytes": (c_size, [ctypes.POINTER(MlpDesc), c_i64]),
     "pnr_mlp_backward_bias": (c_i32, [ctypes.POINTER(MlpDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
                                       c_vp, c_vp, c_size, c_vp]),
+    "pnr_mlp_backward_views": (c_i32, [ctypes.POINTER(MlpDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_vp,
+                                       c_vp, c_vp, c_vp, c_size, c_vp]),
     "pnr_weight_grad_workspace_bytes": (c_size, [c_i32, c_i64]),
     "pnr_weight_grad": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i32, c_i64,
                                 c_vp, c_size, c_vp]),

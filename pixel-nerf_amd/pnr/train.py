@@ -26,8 +26,8 @@ Several source views per object (train.py -V, the DTU setting) are supported: th
 activation save holds one row per (view, point) for the stages before combine_layer, the
 backward sends dL/d(view mean) / NS to every view there (util.combine_interleaved,
 util.py:461-471) and the input-stage backward scatters into each view's latent.  The fused
-f16x3 backward chain (``pnr_mlp_backward``) covers one view; with more, the ResnetFC
-backward runs as per-layer GEMMs (``mlp_backward``) for either forward arithmetic.
+f16x3 backward chain (``pnr_mlp_backward_views``) covers any number of views; the fp32 / bf16
+arithmetics run the ResnetFC backward as per-layer GEMMs (``mlp_backward``).
 """
 import torch
 
@@ -164,51 +164,63 @@ def _tall_mm(a, b):
     return (a.view(s, P // s, a.shape[1]).transpose(1, 2) @ b.view(s, P // s, b.shape[1])).sum(0)
 
 
-def mlp_backward_fused(mlp, code, precision, save, d_o, P):
+def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1):
     """``mlp_backward`` for f16x3 models: the input-gradient chain (masks, residual adds,
-    every 512-wide W^T GEMM, the summed latent gradient) runs in one ``pnr_mlp_backward_bias``
-    launch on the forward's split-fp16 GEMM, which also sums every layer's output gradient
-    over the points (the bias gradients, without re-reading dy); the 512-wide weight
-    gradients are one ``pnr_weight_grad`` launch (split-bf16, fp32-level) over its per-layer
-    output gradients and the activation save."""
+    every 512-wide W^T GEMM, the summed latent gradient, the view mean's backward for ``ns``
+    source views) runs in one ``pnr_mlp_backward_views`` launch on the forward's split-fp16
+    GEMM, which also sums every layer's output gradient over its rows (the bias gradients,
+    without re-reading dy); the 512-wide weight gradients are ``pnr_weight_grad`` launches
+    (split-bf16, fp32-level), one per row count (ns P view rows before combine_layer, P
+    after), over its per-layer output gradients and the activation save."""
     desc, packed, packed_t = mlp.packed_t(code, precision)
     nb = mlp.n_blocks
+    nc = min(mlp.combine_layer, nb) if ns > 1 else nb
     lin_z = list(getattr(mlp, "lin_z", []))
-    feat, z, slot = _save_views(save, P, nb)
+    R = ns * P
+    feat, z, slot = _save_views(save, P, nb, ns=ns)
     dev = d_o.device
     d_o = d_o.contiguous()
-    dy = torch.empty(2 * nb + 1, P, 512, dtype=torch.float32, device=dev)
-    dzl = torch.empty(P, 512, dtype=torch.float32, device=dev) if lin_z else None
+    dy = torch.empty(2 * nb + 1, R, 512, dtype=torch.float32, device=dev)
+    dzl = torch.empty(R, 512, dtype=torch.float32, device=dev) if lin_z else None
     w_out = mlp.lin_out.weight.detach().float().contiguous()
     sums = torch.empty(2 * nb + 1, 512, dtype=torch.float32, device=dev)   # bias gradients, dy's slot order
     lib = _lib.load()
     wsb = lib.pnr_mlp_backward_workspace_bytes(desc, P)
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
-    _lib.check(lib.pnr_mlp_backward_bias(desc, _lib.ptr(packed), _lib.ptr(packed_t), _lib.ptr(w_out), _lib.ptr(save),
-                                         _lib.ptr(d_o), P, _lib.ptr(dy), _lib.ptr(dzl), _lib.ptr(sums), _lib.ptr(ws),
-                                         wsb, _lib.stream_of(dev)),
-               "pnr_mlp_backward_bias")
+    _lib.check(lib.pnr_mlp_backward_views(desc, _lib.ptr(packed), _lib.ptr(packed_t), _lib.ptr(w_out),
+                                          _lib.ptr(save), _lib.ptr(d_o), P, ns, _lib.ptr(dy), _lib.ptr(dzl),
+                                          _lib.ptr(sums), _lib.ptr(ws), wsb, _lib.stream_of(dev)),
+               "pnr_mlp_backward_views")
     g = {}
-    xf = slot(2 * nb)
+    xf = slot(2 * nb, P)
     g[mlp.lin_out.weight] = _tall_mm(d_o, xf)
     g[mlp.lin_out.bias] = d_o.sum(0)
-    acts = save[P * (64 + 512): P * (64 + 512) + 2 * nb * P * 512].view(2 * nb, P, 512)
-    # one pnr_weight_grad launch: fc_0 (dY^T relu(x_b)), fc_1 (dY^T relu(h_b)), lin_z (dY^T z)
-    nz = len(lin_z)
-    gw = weight_grad([dy[b] for b in range(nb)] + [dy[nb + 1 + b] for b in range(nb)] +
-                     [dy[nb + b] for b in range(nz)],
-                     [acts[b] for b in range(nb)] + [acts[nb + b] for b in range(nb)] + [z] * nz, P)
+    # weight gradients grouped by row count: fc_0 (dY^T relu(x_b)), fc_1 (dY^T relu(h_b)),
+    # lin_z (dY^T z)
+    jobs = {}
     for b, blk in enumerate(mlp.blocks):
-        g[blk.fc_0.weight], g[blk.fc_0.bias] = gw[b], sums[b]
-        g[blk.fc_1.weight], g[blk.fc_1.bias] = gw[nb + b], sums[nb + 1 + b]
+        rows = R if b < nc else P
+        jobs.setdefault(rows, []).extend([(blk.fc_0.weight, dy[b, :rows], slot(b, rows)),
+                                          (blk.fc_1.weight, dy[nb + 1 + b, :rows], slot(nb + b, rows))])
     for b, lz in enumerate(lin_z):
-        g[lz.weight] = gw[2 * nb + b]
+        rows = R if b < nc else P
+        jobs.setdefault(rows, []).append((lz.weight, dy[nb + b, :rows], z[:rows]))
+    for rows, js in jobs.items():
+        for i in range(0, len(js), 16):   # pnr_weight_grad: up to 16 layers per launch
+            part = js[i:i + 16]
+            gw = weight_grad([d for _, d, _ in part], [x for _, _, x in part], rows)
+            for j, (param, _, _) in enumerate(part):
+                g[param] = gw[j]
+    for b, blk in enumerate(mlp.blocks):
+        g[blk.fc_0.bias] = sums[b]
+        g[blk.fc_1.bias] = sums[nb + 1 + b]
+    for b, lz in enumerate(lin_z):
         g[lz.bias] = sums[nb + b]
     dx = dy[nb]
     d_in = mlp.lin_in.weight.shape[1]
     g[mlp.lin_in.weight] = _tall_mm(dx, feat)[:, :d_in]
     g[mlp.lin_in.bias] = sums[nb]
-    d_feat = torch.zeros(P, 64, device=dev, dtype=torch.float32)
+    d_feat = torch.zeros(R, 64, device=dev, dtype=torch.float32)
     d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
     return g, d_feat, dzl
 
@@ -257,8 +269,8 @@ class RenderPoints(torch.autograd.Function):
         d_o = torch.cat([d_out[:, :3] * out[:, :3] * (1.0 - out[:, :3]),
                          d_out[:, 3:] * (out[:, 3:] > 0)], dim=1)
         ns = net.num_views_per_obj
-        if net.mlp_precision == "f16x3" and ns == 1:
-            g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P)
+        if net.mlp_precision == "f16x3":
+            g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns)
         else:
             g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns, use_wgrad=net.mlp_precision == "f16x3")
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]

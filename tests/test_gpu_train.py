@@ -278,19 +278,20 @@ def test_training_noise_std_draw_order_matches_reference():
     assert torch.isfinite(lat.grad).all()
 
 
-@pytest.mark.parametrize("rays_per_obj,K", [(96, 41), (256, 64)])
-def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K):
-    """pnr_mlp_backward_bias (the f16x3 W^T chain: masks, residuals, lin_z latent gradient,
-    bias column sums) plus the batched weight GEMMs against the per-layer fp32 torch backward
-    (train.mlp_backward) on the same activation save: 7,872 points (ragged last tile, one
-    tile per workgroup) and 32,768 (several tiles per workgroup: the bias partials add up
-    across tiles), per-point gradient magnitudes spread over 2^-20 .. 1.  Tolerance 2e-5 of
-    each tensor's max-abs."""
+@pytest.mark.parametrize("rays_per_obj,K,ns", [(96, 41, 1), (256, 64, 1), (40, 41, 3), (256, 64, 2)])
+def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K, ns):
+    """pnr_mlp_backward_views (the f16x3 W^T chain: masks, residuals, lin_z latent gradient,
+    bias column sums, the view mean's backward) plus the batched weight GEMMs against the
+    per-layer fp32 torch backward (train.mlp_backward) on the same activation save: 7,872
+    points (ragged last tile, one tile per workgroup), 32,768 (several tiles per workgroup: the
+    bias partials add up across tiles), and NS = 3 / 2 source views per point (the DTU
+    setting: per-view rows before combine_layer), per-point gradient magnitudes spread over
+    2^-20 .. 1.  Tolerance 2e-5 of each tensor's max-abs."""
     from types import SimpleNamespace
 
     from pnr import train
 
-    cs = case(sb=2, rays_per_obj=rays_per_obj, kc=K)
+    cs = case(sb=2, rays_per_obj=rays_per_obj, kc=K, ns=ns)
     net = PixelNeRFNet(conf())
     net.load_state_dict(cs["sd"], strict=False)
     net = net.to(DEV)
@@ -311,8 +312,9 @@ def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K):
     d_o = torch.randn(P, 4, generator=gen) * torch.exp2(-20.0 * torch.rand(P, 1, generator=gen))
     d_o = d_o.to(DEV)
     with torch.no_grad():
-        g_ref, df_ref, dz_ref = train.mlp_backward(net.mlp_coarse, save, d_o, P)
-        g, df, dz = train.mlp_backward_fused(net.mlp_coarse, net.code, "f16x3", save, d_o, P)
+        assert net.num_views_per_obj == ns
+        g_ref, df_ref, dz_ref = train.mlp_backward(net.mlp_coarse, save, d_o, P, ns)
+        g, df, dz = train.mlp_backward_fused(net.mlp_coarse, net.code, "f16x3", save, d_o, P, ns)
     worst = 0.0
     pairs = [(g[p], g_ref[p]) for p in g_ref] + [(df, df_ref), (dz, dz_ref)]
     for a, b in pairs:
