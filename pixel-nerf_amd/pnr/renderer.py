@@ -258,9 +258,12 @@ class NeRFRenderer(torch.nn.Module):
         if streams is None:
             seed = int(torch.randint(0, 2 ** 63 - 1, (1,), dtype=torch.int64).item())
             self.last_seed = seed   # the counter-mode key of the last call (tests replay it)
-        # one object: ray chunks of max_rays_per_call (several objects: one call, the scene
-        # record covers them all)
-        step = max(1, int(self.max_rays_per_call)) if sb == 1 else max(B, 1)
+        # one object: ray chunks of at most eval_batch_size rays (the reference bounds a model
+        # call to eval_batch_size points, nerf.py:191-201; the fused march keeps no per-point
+        # activations in HBM, so the bound is on rays: its workspace is ~4 KB per ray) and
+        # max_rays_per_call.  Several objects: one call, the scene record covers them all
+        # (chunking inside each object would move the rays' counter-mode draw indices).
+        step = max(1, min(int(self.max_rays_per_call), int(self.eval_batch_size))) if sb == 1 else max(B, 1)
         parts = []
         for r0 in range(0, max(B, 1), step):
             r1 = min(B, r0 + step)

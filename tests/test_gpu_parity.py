@@ -269,6 +269,56 @@ def test_point_query_dynamic_range(precision, lat_scale, w_scale, latent_proj):
                  atol=ATOL * max(1.0, mag))
 
 
+def heavy_tailed_state(seed):
+    """Trained-like weight statistics for the accuracy check of the split arithmetics: every
+    ResnetFC matrix gets log-normal row and column scales (exp(1.5 N), a ~e^+-4.5 spread per
+    side) and 0.2 % outlier entries x 30, then is renormalised to its original Frobenius norm
+    so activations stay O(1); the latent gets log-normal per-channel scales (exp(2 N))."""
+    sd = synth.pixelnerf_state(seed)
+    g = torch.Generator().manual_seed(seed)
+    for k in sorted(sd):
+        v = sd[k]
+        if not k.endswith("weight") or v.dim() != 2 or not k.startswith("mlp_"):
+            continue
+        r = torch.exp(1.5 * torch.randn(v.shape[0], 1, generator=g))
+        c = torch.exp(1.5 * torch.randn(1, v.shape[1], generator=g))
+        w = v * r * c
+        out = torch.rand(v.shape, generator=g) < 0.002
+        w = torch.where(out, w * 30.0, w)
+        sd[k] = (w * (v.norm() / w.norm().clamp_min(1e-30))).contiguous()
+    return sd
+
+
+@pytest.mark.parametrize("latent_proj", [True, False])
+@pytest.mark.parametrize("precision", PRECS)
+def test_point_query_heavy_tailed_weights(precision, latent_proj):
+    """the split arithmetics (f16x3: per-layer weight scale, per-column
+    image scales; bf16x6 / x9) on heavy-tailed, trained-like weights and latent channels
+    (heavy_tailed_state) against the fp32 oracle, tolerance relative to the output magnitude
+    as in test_point_query_dynamic_range."""
+    sd = heavy_tailed_state(21)
+    ch = torch.exp(2.0 * torch.randn(512, generator=torch.Generator().manual_seed(3)))
+    lat = synth.latent(12, 1, 512, 16, 16) * ch[None, :, None, None]
+    poses = synth.srn_poses([10.0])
+    focal = torch.tensor(40.0)
+    xyz = torch.from_numpy(synth.hash_sym(93, (1, 512, 3), 0.5))
+    vd = torch.nn.functional.normalize(torch.from_numpy(synth.hash_sym(94, (1, 512, 3), 1.0)), dim=-1)
+    scene = ref_cpu.Scene(lat, poses, focal, 64, 64, None)
+    with torch.no_grad():
+        ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, True, vd)
+    net = PixelNeRFNet(model_conf())
+    net.mlp_precision = precision
+    net.use_latent_proj = latent_proj
+    net.load_state_dict(sd, strict=False)
+    net = net.to(DEV).eval()
+    net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (64, 64))
+    with torch.no_grad():
+        out = net(xyz.to(DEV), coarse=True, viewdirs=vd.to(DEV)).cpu()
+    mag = float(ref.abs().max())
+    assert torch.isfinite(out).all() and float(ref[..., 3].abs().max()) > 0   # sigma not all clipped
+    assert_close(out, ref, "heavy-tailed weights", atol=ATOL * max(1.0, mag))
+
+
 @pytest.mark.parametrize("latent_proj", [True, False])
 @pytest.mark.parametrize("precision", ["fp32", "f16x3"])
 def test_point_query_camera_plane_and_behind_camera(precision, latent_proj):

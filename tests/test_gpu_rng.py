@@ -106,9 +106,13 @@ def test_counter_render_is_chunk_invariant():
     _, whole = render(net, sc["rays"][None], 64, 64)
     torch.manual_seed(5)
     _, chunked = render(net, sc["rays"][None], 64, 64, max_rays=100)
+    # eval_batch_size bounds a call's rays the same way (the reference's chunk knob)
+    torch.manual_seed(5)
+    _, ebs = render(net, sc["rays"][None], 64, 64, eval_batch_size=96)
     for p in ("coarse", "fine"):
         for k in ("rgb", "depth", "weights", "z"):
             assert torch.equal(whole[p][k], chunked[p][k]), (p, k)
+            assert torch.equal(whole[p][k], ebs[p][k]), (p, k, "eval_batch_size")
 
 
 def test_counter_draw_distribution():
