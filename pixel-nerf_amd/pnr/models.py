@@ -166,8 +166,15 @@ class ResnetFC(nn.Module):
         return w, keep
 
     def _pack_key(self, code, precision):
-        params = [p for p in self.parameters()] + [code._freqs, code._phases]
-        return (precision,) + tuple((p.data_ptr(), p._version) for p in params)
+        # the submodule list is cached (nn.Module.parameters() walks and de-duplicates the
+        # tree on every call: ~50 us of host time per MLP per render call); each submodule's
+        # _parameters dict is read live, so a reassigned parameter still changes the key
+        snap = self.__dict__.get("_pnr_mods")
+        if snap is None or any(tuple(m._modules.values()) != kids for m, kids in snap):   # submodule swapped
+            snap = [(m, tuple(m._modules.values())) for m in self.modules()]
+            self.__dict__["_pnr_mods"] = snap
+        params = [p for m, _ in snap for p in m._parameters.values() if p is not None]
+        return (precision,) + tuple((p.data_ptr(), p._version) for p in params + [code._freqs, code._phases])
 
     def packed(self, code, precision="fp32"):
         """Packed fragment-order copy of the weights (re-packed when they change).  The
