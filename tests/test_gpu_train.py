@@ -21,15 +21,15 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def conf():
-    mlp = dict(type="resnet", n_blocks=5, d_hidden=512, combine_layer=3, combine_type="average")
+def conf(combine_layer=3):
+    mlp = dict(type="resnet", n_blocks=5, d_hidden=512, combine_layer=combine_layer, combine_type="average")
     return dict(use_encoder=True, use_xyz=True, use_code=True,
                 code=dict(num_freqs=6, freq_factor=1.5, include_input=True), use_viewdirs=True,
                 use_code_viewdirs=False, mlp_coarse=dict(mlp), mlp_fine=dict(mlp),
                 encoder=dict(backbone="resnet34", pretrained=False, num_layers=4))
 
 
-def case(sb=2, rays_per_obj=8, kc=32, kf=24, kfd=8, seed=3, ns=1):
+def case(sb=2, rays_per_obj=8, kc=32, kf=24, kfd=8, seed=3, ns=1, combine_layer=3):
     sc = synth.scene_multiview(seed=seed, n_views=sb * ns, n_rays=sb * rays_per_obj, channels=512,
                                h_l=12, w_l=14)
     poses = sc["poses"].reshape(sb, ns, 4, 4) if ns > 1 else sc["poses"].reshape(sb, 4, 4)
@@ -39,7 +39,7 @@ def case(sb=2, rays_per_obj=8, kc=32, kf=24, kfd=8, seed=3, ns=1):
     B = sb * rays_per_obj
     streams = synth.rng_streams(seed + 1, B, kc, kf, kfd)
     target = torch.from_numpy(synth.hash_uniform(seed + 2, B * 3).astype("float32")).reshape(sb, -1, 3)
-    return dict(sd=synth.pixelnerf_state(seed + 4), latent=sc["latent"], poses=poses, focal=focal, c=c,
+    return dict(sd=synth.pixelnerf_state(seed + 4, combine_layer=combine_layer), latent=sc["latent"], poses=poses, focal=focal, c=c,
                 rays=rays, streams=streams, target=target, kc=kc, kf=kf, kfd=kfd,
                 width=sc["width"], height=sc["height"])
 
@@ -278,21 +278,23 @@ def test_training_noise_std_draw_order_matches_reference():
     assert torch.isfinite(lat.grad).all()
 
 
-@pytest.mark.parametrize("rays_per_obj,K,ns", [(96, 41, 1), (256, 64, 1), (40, 41, 3), (256, 64, 2)])
-def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K, ns):
+@pytest.mark.parametrize("rays_per_obj,K,ns,comb", [(96, 41, 1, 3), (256, 64, 1, 3), (40, 41, 3, 3), (256, 64, 2, 3),
+                                                     (40, 41, 3, 2)])
+def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K, ns, comb):
     """pnr_mlp_backward_views (the f16x3 W^T chain: masks, residuals, lin_z latent gradient,
     bias column sums, the view mean's backward) plus the batched weight GEMMs against the
     per-layer fp32 torch backward (train.mlp_backward) on the same activation save: 7,872
     points (ragged last tile, one tile per workgroup), 32,768 (several tiles per workgroup: the
     bias partials add up across tiles), and NS = 3 / 2 source views per point (the DTU
     setting: per-view rows before combine_layer), per-point gradient magnitudes spread over
-    2^-20 .. 1.  Tolerance 2e-5 of each tensor's max-abs."""
+    2^-20 .. 1; combine_layer 2 as well as the default 3.  Tolerance 2e-5 of each tensor's
+    max-abs."""
     from types import SimpleNamespace
 
     from pnr import train
 
-    cs = case(sb=2, rays_per_obj=rays_per_obj, kc=K, ns=ns)
-    net = PixelNeRFNet(conf())
+    cs = case(sb=2, rays_per_obj=rays_per_obj, kc=K, ns=ns, combine_layer=comb)
+    net = PixelNeRFNet(conf(comb))
     net.load_state_dict(cs["sd"], strict=False)
     net = net.to(DEV)
     net.mlp_precision = "f16x3"

@@ -210,3 +210,20 @@ def test_pack_key_tracks_weight_changes():
     assert k2 != k1
     m.blocks[2] = copy.deepcopy(m.blocks[2])
     assert m._pack_key(net.code, "f16x3") != k2
+
+
+def test_render_set_fused_modes():
+    """pnr_render_set_fused (host state only, no device work): default 2, returns the previous
+    mode, out-of-range values select the default; pnr._lib.fused_march restores the mode."""
+    lib = _lib.load()
+    prev = lib.pnr_render_set_fused(2)
+    try:
+        assert lib.pnr_render_set_fused(0) == 2
+        assert lib.pnr_render_set_fused(1) == 0
+        assert lib.pnr_render_set_fused(7) == 1     # invalid -> default
+        assert lib.pnr_render_set_fused(2) == 2
+        with _lib.fused_march(0):
+            assert lib.pnr_render_set_fused(0) == 0
+        assert lib.pnr_render_set_fused(2) == 2
+    finally:
+        lib.pnr_render_set_fused(prev)
