@@ -782,6 +782,7 @@ def test_torch_ops_render_rays_matches_fixture(name):
     (128, 0, 0, True, False, 1, 1),      # two tiles per ray
     (32, 32, 0, True, False, 1, 1),      # coarse K = 32 separate, fine K = 64 fused
     (64, 64, 16, False, False, 3, 2),    # multi-view mean, two objects, depth samples
+    (64, 64, 16, True, True, 1, 1),      # lindisp + depth samples, per-ray near / far
 ])
 def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_views, sb):
     """The fused ray march (pnr_render_set_fused: mode 2, the default, sampling + MLP + composite
@@ -798,6 +799,11 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
     if n_views == 1 and sb == 1:
         sc = synth.scene_srn(seed=5, n_rays=n_rays, pick="all")
         lat, poses, focal, wh, c, rays = sc["latent"], sc["poses"], sc["focal"], (128, 128), None, sc["rays"]
+        if lindisp:   # per-ray near / far (the fused epilogue reads them from LDS per ray)
+            rays = rays.clone()
+            h = torch.from_numpy(synth.hash_uniform(17, n_rays).astype("float32"))
+            rays[:, 6] = 0.2 + 0.6 * h
+            rays[:, 7] = 2.5 + 1.5 * h
     else:
         lat = synth.latent(10, sb * n_views, 512, 30, 40)
         poses = synth.srn_poses([30.0 * i for i in range(sb * n_views)], radius=1.4).reshape(sb, n_views, 4, 4)
