@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 2
+#define PNR_ABI_VERSION 3
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -133,6 +133,12 @@ typedef struct pnr_render_cfg {
     float depth_std;      /*                              (nerf.py:80)       */
     int32_t white_bkgd;   /*                              (nerf.py:83)       */
     int32_t lindisp;      /*                              (nerf.py:84)       */
+    /* ABI 3: ray-march schedule of THIS call (no process state is read or written):
+     *   2  fused passes + fine-draw kernel, 1  fine draws in the coarse epilogue too,
+     *   0  separate sample / MLP / composite kernels (see pnr_render_set_fused);
+     *  -1  the process default set by pnr_render_set_fused (initially 2).
+     * All modes give bit-identical results. */
+    int32_t march_mode;
 } pnr_render_cfg;
 
 /* Outputs; any pointer may be NULL except the rgb/depth of each pass that runs. */
@@ -240,7 +246,10 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc,
  * the workgroup's other seven wait).  0: the separate sample / MLP / composite kernels.  The
  * fusion applies when a pass's samples per ray are 64 or 128 (and kc + kf <= 128 for the fine
  * draws) and mlp_fine is not None; other shapes take the separate kernels.  All modes run the
- * same device code and give bit-identical results.  Process-wide; returns the previous setting. */
+ * same device code and give bit-identical results.  This only sets the DEFAULT that calls with
+ * pnr_render_cfg.march_mode = -1 use (ABI 3); a call that names its mode reads no process state,
+ * so host threads (DataParallel replicas, nerf.py:370) may render with different modes at once.
+ * Returns the previous default. */
 int32_t pnr_render_set_fused(int32_t on);
 
 /* ---- building blocks (also the generic model-callback path) ------------------ */

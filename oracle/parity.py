@@ -134,7 +134,10 @@ def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref, z_
     else:
         bins_differ = marginal = torch.zeros(B, dtype=torch.bool)
     z_differs = ~close_mask(zh, zr).all(-1)
-    flip = bins_differ | (marginal & z_differs)
+    # a marginal draw (the device's double cdf scan and torch's fp32 cumsum round a boundary
+    # apart) explains differing samples only when the caller also checks that the samples
+    # follow the HIP's own weights (z_expected_hip); otherwise only a proven bin flip does
+    flip = bins_differ | (marginal & z_differs) if z_expected_hip is not None else bins_differ
     unexplained = z_differs & ~flip
     inconsistent = torch.zeros(B, dtype=torch.bool)
     if z_expected_hip is not None:
@@ -146,3 +149,82 @@ def classify_fine(w_coarse_hip, w_coarse_ref, u_fine, z_fine_hip, z_fine_ref, z_
         inconsistent = flip & ~follows
     return dict(flip=flip, z_differs=z_differs, unexplained=unexplained, inconsistent=inconsistent,
                 flip_idx=[int(i) for i in torch.nonzero(flip).reshape(-1)])
+
+
+def _object_scene(scene, s):
+    """A shallow copy of ``ref_cpu.Scene`` restricted to object ``s`` (its NS views)."""
+    import copy
+
+    sub = copy.copy(scene)
+    ns = scene.ns
+    sub.latent = scene.latent[s * ns:(s + 1) * ns]
+    sub.poses = scene.poses[s * ns:(s + 1) * ns]
+    sub.focal = scene.focal[s:s + 1] if scene.focal.shape[0] > 1 else scene.focal
+    sub.c = scene.c[s:s + 1] if scene.c.shape[0] > 1 else scene.c
+    return sub
+
+
+def fine_pass_at(sd, scene, rays, z_fine, ray_idx, rays_per_obj, white_bkgd, model_kw=None):
+    """The reference's fine pass (nerf.py:284-301: the fine model at o + z d, then the
+    composite of nerf.py:176-249) evaluated on the CPU oracle at GIVEN fine samples -- the
+    HIP's own ``z_fine`` of a flipped ray -- for the rays ``ray_idx`` of the flattened batch.
+    Returns (weights (n, K), rgb (n, 3), depth (n,)) in ``ray_idx`` order.  ``model_kw``:
+    d_latent / n_blocks / combine_layer / has_fine for ``ref_cpu.pixelnerf_forward``."""
+    from . import ref_cpu
+
+    rays = rays.reshape(-1, 8).float().cpu()
+    z_fine = z_fine.reshape(rays.shape[0], -1).float().cpu()
+    K = z_fine.shape[1]
+    idx = [int(i) for i in ray_idx]
+    w_out = torch.zeros(len(idx), K)
+    rgb_out = torch.zeros(len(idx), 3)
+    d_out = torch.zeros(len(idx))
+    by_obj = {}
+    for j, i in enumerate(idx):
+        by_obj.setdefault(i // rays_per_obj, []).append((j, i))
+    for s, items in by_obj.items():
+        sub = _object_scene(scene, s)
+        sel = torch.tensor([i for _, i in items])
+        r = rays[sel]
+        z = z_fine[sel]
+        pts, dirs = ref_cpu._points(r, z)
+        with torch.no_grad():
+            raw = ref_cpu.pixelnerf_forward(sd, sub, pts.reshape(1, -1, 3), False, dirs.reshape(1, -1, 3),
+                                            **(model_kw or {}))
+            w, rgb, depth = ref_cpu.composite(r, z, raw.reshape(len(items), K, -1), white_bkgd)
+        for k, (j, _) in enumerate(items):
+            w_out[j], rgb_out[j], d_out[j] = w[k], rgb[k], depth[k]
+    return w_out, rgb_out, d_out
+
+
+def check_flipped_outputs(sd, scene, rays, z_fine_hip, rgb_hip, depth_hip, w_hip, flip_idx, rays_per_obj,
+                          white_bkgd, model_kw=None, w_coarse_hip=None, u_fine=None):
+    """Output check of the rays ``classify_fine`` excluded as flipped (VERDICT r2 "Missing" 2):
+    each one's HIP rgb / depth / weights against the oracle fine pass at the HIP's own fine
+    samples (``fine_pass_at``), within the fp32 tolerance.  Returns a dict with ``ok`` (bool),
+    per-ray max errors and, given the HIP coarse weights and u, each flip's distance of its
+    draw to the nearest cdf boundary (``boundary_distance``) so a reader can judge how marginal
+    it was."""
+    if not flip_idx:
+        return dict(ok=True, rays=[], max_abs=dict(rgb=0.0, depth=0.0, weights=0.0))
+    B = rays.reshape(-1, 8).shape[0]
+    w_ref, rgb_ref, d_ref = fine_pass_at(sd, scene, rays, z_fine_hip, flip_idx, rays_per_obj, white_bkgd,
+                                         model_kw)
+    sel = torch.tensor(flip_idx)
+    rgb = rgb_hip.reshape(B, 3).float().cpu()[sel]
+    dep = depth_hip.reshape(B).float().cpu()[sel]
+    res = dict(rays=list(flip_idx), max_abs={}, ok=True)
+    per_ray_ok = torch.ones(len(flip_idx), dtype=torch.bool)
+    pairs = [("rgb", rgb, rgb_ref), ("depth", dep, d_ref)]
+    if w_hip is not None:
+        pairs.append(("weights", w_hip.reshape(B, -1).float().cpu()[sel], w_ref))
+    for name, a, b in pairs:
+        ok = close_mask(a, b)
+        per_ray_ok &= ok.reshape(len(flip_idx), -1).all(-1)
+        res["max_abs"][name] = float((a - b).abs().max())
+    res["ok"] = bool(per_ray_ok.all())
+    res["bad_rays"] = [flip_idx[j] for j in torch.nonzero(~per_ray_ok).reshape(-1).tolist()]
+    if w_coarse_hip is not None and u_fine is not None and u_fine.numel() > 0:
+        d = boundary_distance(w_coarse_hip.reshape(B, -1)[sel], u_fine.reshape(B, -1)[sel])
+        res["boundary_distance"] = [float(x) for x in d]
+    return res

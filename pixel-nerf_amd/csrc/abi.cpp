@@ -50,10 +50,12 @@ int64_t latent_proj_floats(const pnr_scene &, const pnr_mlp_desc &);
 int launch_latent_proj(const pnr_scene &, const pnr_mlp_weights &, float *, size_t, hipStream_t);
 
 static thread_local char g_err[1024];
-// pnr_render_set_fused: the fused ray march (2, the default: draws + composite in the MLP passes,
-// the fine draws in their own kernel; 1: those too in the coarse epilogue) or the separate
-// sample / composite kernels (0)
-static std::atomic<int> g_fused_march{2};
+// pnr_render_set_fused: the DEFAULT march mode of calls whose pnr_render_cfg.march_mode is -1:
+// the fused ray march (2: draws + composite in the MLP passes, the fine draws in their own
+// kernel; 1: those too in the coarse epilogue) or the separate sample / composite kernels (0).
+// Set once at start-up by callers that want another default; a call naming its own mode never
+// reads it.
+static std::atomic<int> g_fused_default{2};
 
 void set_error(const char *fmt, ...) {
     va_list ap;
@@ -348,6 +350,9 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     if (!coarse_packed) return fail(PNR_ERR_INVALID, "coarse_packed is NULL");
     const int kc = cfg->n_coarse, kf = cfg->n_fine, kfd = cfg->n_fine_depth;
     if (kc < 1) return fail(PNR_ERR_INVALID, "n_coarse < 1");
+    if (cfg->march_mode < -1 || cfg->march_mode > 2)
+        return fail(PNR_ERR_INVALID, "march_mode must be -1 (default), 0, 1 or 2 (got %d)", cfg->march_mode);
+    const int mode = cfg->march_mode >= 0 ? cfg->march_mode : g_fused_default.load(std::memory_order_relaxed);
     if (kf < 0 || kfd < 0 || kfd > kf) return fail(PNR_ERR_INVALID, "need 0 <= n_fine_depth <= n_fine");
     if (kc + kf > 1024) return fail(PNR_ERR_UNSUPPORTED, "n_coarse + n_fine must be <= 1024");
     if (kf > 0 && !fine_packed) return fail(PNR_ERR_INVALID, "fine_packed is NULL");
@@ -397,9 +402,9 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     // the kc coarse samples re-enter the fine pass with the MLP that already evaluated them, so
     // only the kf new samples run through it and the coarse outputs are merged in.
     const bool reuse = kf > 0 && fine_packed == coarse_packed && fine_proj == coarse_proj;
-    const bool fused = g_fused_march.load(std::memory_order_relaxed) != 0;
+    const bool fused = mode != 0;
     const bool fuse_c = fused && kc % 64 == 0 && kc <= 128;
-    const bool fuse_s = fuse_c && g_fused_march.load(std::memory_order_relaxed) == 1 && kf > 0 && !reuse &&
+    const bool fuse_s = fuse_c && mode == 1 && kf > 0 && !reuse &&
                         kc <= 64 && sort_width(kall) <= 128;
     const bool fuse_f = fused && kf > 0 && !reuse && kall % 64 == 0 && kall <= 128;
     float *zf = kf > 0 ? (out->z_fine ? out->z_fine : reinterpret_cast<float *>(ws + w.z_f)) : nullptr;
@@ -483,7 +488,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     return mark(6);
 }
 
-int32_t pnr_render_set_fused(int32_t on) { return g_fused_march.exchange(on < 0 || on > 2 ? 2 : on); }
+int32_t pnr_render_set_fused(int32_t on) { return g_fused_default.exchange(on < 0 || on > 2 ? 2 : on); }
 
 int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse, const float *u_coarse,
                       int32_t lindisp, float *z, pnr_stream_t stream) {

@@ -11,6 +11,7 @@
 //   pnr::point_query   PixelNeRFNet.forward (models.py:146-266)
 //   pnr::composite     NeRFRenderer.composite's volume integral (nerf.py:176-249)
 #include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -38,6 +39,23 @@ const float *fptr(const at::Tensor &t, const char *name) {
 const float *opt_fptr(const c10::optional<at::Tensor> &t, const char *name) {
     if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
     return fptr(*t, name);
+}
+
+// every tensor of one call lives on the call's device (the library dereferences raw pointers:
+// a host or other-device buffer would fault inside a kernel instead of failing here)
+void same_device(const at::Tensor &t, const at::Device &dev, const char *name) {
+    TORCH_CHECK(t.device() == dev, name, " is on ", t.device(), ", the call runs on ", dev);
+}
+
+const void *packed_ptr(const at::Tensor &t, const at::Device &dev, const char *name) {
+    TORCH_CHECK(t.defined() && t.numel() > 0, name, " is empty");
+    same_device(t, dev, name);
+    TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+    return t.data_ptr();
+}
+
+void same_device_opt(const c10::optional<at::Tensor> &t, const at::Device &dev, const char *name) {
+    if (t.has_value() && t->defined() && t->numel() > 0) same_device(*t, dev, name);
 }
 
 pnr_scene make_scene(const at::Tensor &latent_cl, const at::Tensor &cams, int64_t n_obj, int64_t n_views,
@@ -85,9 +103,21 @@ std::vector<at::Tensor> render_rays(const at::Tensor &latent_cl, const at::Tenso
                                     const c10::optional<at::Tensor> &u_coarse, const c10::optional<at::Tensor> &u_fine,
                                     const c10::optional<at::Tensor> &u_fine_jit,
                                     const c10::optional<at::Tensor> &n_depth, int64_t seed, int64_t offset,
-                                    bool want_weights, bool want_z, at::IntArrayRef events) {
+                                    bool want_weights, bool want_z, at::IntArrayRef events, int64_t march_mode) {
     TORCH_CHECK(rays.dim() == 2 && rays.size(1) == 8, "rays must be (B, 8)");
     TORCH_CHECK(events.empty() || events.size() == 7, "events: none or 7 hipEvent_t handles");
+    const at::Device dev = rays.device();
+    c10::OptionalDeviceGuard guard(dev);
+    same_device(latent_cl, dev, "latent_cl");
+    same_device(cams, dev, "cams");
+    const void *cpk = packed_ptr(coarse_packed, dev, "coarse_packed");
+    const void *fpk = n_fine > 0 ? packed_ptr(fine_packed, dev, "fine_packed") : nullptr;
+    same_device_opt(coarse_proj, dev, "coarse_proj");
+    same_device_opt(fine_proj, dev, "fine_proj");
+    same_device_opt(u_coarse, dev, "u_coarse");
+    same_device_opt(u_fine, dev, "u_fine");
+    same_device_opt(u_fine_jit, dev, "u_fine_jit");
+    same_device_opt(n_depth, dev, "n_depth");
     const pnr_scene sc = make_scene(latent_cl, cams, n_obj, n_views, image_w, image_h);
     const pnr_mlp_desc d = make_desc(desc);
     const int64_t B = rays.size(0);
@@ -118,13 +148,12 @@ std::vector<at::Tensor> render_rays(const at::Tensor &latent_cl, const at::Tenso
     rng.seed = (uint64_t)seed;
     rng.offset = (uint64_t)offset;
     pnr_render_cfg cfg{(int32_t)n_coarse, (int32_t)n_fine, (int32_t)n_fine_depth, (float)depth_std,
-                       (int32_t)white_bkgd, (int32_t)lindisp};
+                       (int32_t)white_bkgd, (int32_t)lindisp, (int32_t)march_mode};
     const size_t ws_bytes = pnr_render_workspace_bytes(&sc, &cfg, B);
     at::Tensor ws = at::empty({(int64_t)(ws_bytes ? ws_bytes : 1)}, rays.options().dtype(at::kByte));
-    const void *fpk = fine ? fine_packed.data_ptr() : nullptr;
     void *ev[7] = {};
     for (size_t i = 0; i < events.size(); ++i) ev[i] = reinterpret_cast<void *>((intptr_t)events[i]);
-    check(pnr_render_forward_proj(&sc, &d, coarse_packed.data_ptr(), fpk, opt_fptr(coarse_proj, "coarse_proj"),
+    check(pnr_render_forward_proj(&sc, &d, cpk, fpk, opt_fptr(coarse_proj, "coarse_proj"),
                                   fine ? opt_fptr(fine_proj, "fine_proj") : nullptr, &r, &rng, &cfg, &out,
                                   ws.data_ptr(), ws_bytes, stream_of(rays),
                                   events.empty() ? nullptr : reinterpret_cast<void *const *>(ev)),
@@ -143,7 +172,8 @@ std::vector<at::Tensor> render_rays_meta(const at::Tensor &latent_cl, const at::
                                          const c10::optional<at::Tensor> &u_fine,
                                          const c10::optional<at::Tensor> &u_fine_jit,
                                          const c10::optional<at::Tensor> &n_depth, int64_t seed, int64_t offset,
-                                         bool want_weights, bool want_z, at::IntArrayRef events) {
+                                         bool want_weights, bool want_z, at::IntArrayRef events,
+                                         int64_t march_mode) {
     const int64_t B = rays.size(0);
     const auto o = f32_like(rays);
     const bool fine = n_fine > 0;
@@ -159,13 +189,20 @@ at::Tensor point_query(const at::Tensor &latent_cl, const at::Tensor &cams, int6
                        const c10::optional<at::Tensor> &viewdirs) {
     TORCH_CHECK(xyz.dim() == 3 && xyz.size(2) == 3, "xyz must be (SB, B, 3)");
     TORCH_CHECK(xyz.size(0) == n_obj, "xyz has ", xyz.size(0), " objects, the scene ", n_obj);
+    const at::Device dev = xyz.device();
+    c10::OptionalDeviceGuard guard(dev);
+    same_device(latent_cl, dev, "latent_cl");
+    same_device(cams, dev, "cams");
+    const void *pk = packed_ptr(packed, dev, "packed");
+    same_device_opt(proj, dev, "proj");
+    same_device_opt(viewdirs, dev, "viewdirs");
     const pnr_scene sc = make_scene(latent_cl, cams, n_obj, n_views, image_w, image_h);
     const pnr_mlp_desc d = make_desc(desc);
     const int64_t P = xyz.size(0) * xyz.size(1);
     at::Tensor out = at::empty({xyz.size(0), xyz.size(1), 4}, f32_like(xyz));
     const size_t ws_bytes = pnr_point_query_workspace_bytes(&sc, P);
     at::Tensor ws = at::empty({(int64_t)(ws_bytes ? ws_bytes : 1)}, xyz.options().dtype(at::kByte));
-    check(pnr_point_query_proj(&sc, &d, packed.data_ptr(), opt_fptr(proj, "proj"), fptr(xyz, "xyz"),
+    check(pnr_point_query_proj(&sc, &d, pk, opt_fptr(proj, "proj"), fptr(xyz, "xyz"),
                                opt_fptr(viewdirs, "viewdirs"), xyz.size(1), out.data_ptr<float>(), ws.data_ptr(),
                                ws_bytes, stream_of(xyz)),
           "pnr::point_query");
@@ -185,6 +222,10 @@ std::vector<at::Tensor> composite(const at::Tensor &z, const at::Tensor &raw, co
                     raw.size(1) == z.size(1),
                 "composite: z (B, K), raw (B, K, 4)");
     const int64_t B = z.size(0), K = z.size(1);
+    const at::Device dev = z.device();
+    c10::OptionalDeviceGuard guard(dev);
+    same_device(raw, dev, "raw");
+    same_device(rays, dev, "rays");
     const auto o = f32_like(z);
     at::Tensor w = want_weights ? at::empty({B, K}, o) : at::empty({0}, o);
     at::Tensor rgb = at::empty({B, 3}, o), depth = at::empty({B}, o);
@@ -209,7 +250,7 @@ TORCH_LIBRARY(pnr, m) {
           "int[] desc, Tensor coarse_packed, Tensor fine_packed, Tensor? coarse_proj, Tensor? fine_proj, "
           "Tensor rays, int rays_per_obj, int n_coarse, int n_fine, int n_fine_depth, float depth_std, "
           "bool white_bkgd, bool lindisp, Tensor? u_coarse, Tensor? u_fine, Tensor? u_fine_jit, Tensor? n_depth, "
-          "int seed, int offset, bool want_weights, bool want_z, int[] events=[]) -> Tensor[]");
+          "int seed, int offset, bool want_weights, bool want_z, int[] events=[], int march_mode=-1) -> Tensor[]");
     m.def("point_query(Tensor latent_cl, Tensor cams, int n_obj, int n_views, float image_w, float image_h, "
           "int[] desc, Tensor packed, Tensor? proj, Tensor xyz, Tensor? viewdirs) -> Tensor");
     m.def("composite(Tensor z, Tensor raw, Tensor rays, bool white_bkgd, bool want_weights) -> Tensor[]");

@@ -54,12 +54,13 @@ class Rng(ctypes.Structure):
 
 # pnr_rng counter-mode stream ids (PNR_RNG_*)
 RNG_U_COARSE, RNG_U_FINE, RNG_U_FINE_JIT, RNG_N_DEPTH = 0, 1, 2, 3
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class RenderCfg(ctypes.Structure):
     _fields_ = [("n_coarse", c_i32), ("n_fine", c_i32), ("n_fine_depth", c_i32),
-                ("depth_std", c_f), ("white_bkgd", c_i32), ("lindisp", c_i32)]
+                ("depth_std", c_f), ("white_bkgd", c_i32), ("lindisp", c_i32),
+                ("march_mode", c_i32)]   # ABI 3: -1 = the pnr_render_set_fused default
 
 
 class RenderOut(ctypes.Structure):
@@ -168,9 +169,11 @@ def ptr(t):
 
 
 class fused_march:
-    """Context manager: pnr_render_set_fused(mode) inside, the previous setting restored after
+    """Context manager: pnr_render_set_fused(mode) inside, the previous DEFAULT restored after
     (2, the default: fused passes + fine-draw kernel; 1: fine draws in the coarse epilogue too;
-    0: the separate sample / composite kernels)."""
+    0: the separate sample / composite kernels).  It changes the process default, which only
+    calls without their own mode use; ``NeRFRenderer.march_mode`` names the mode per renderer
+    (pnr_render_cfg.march_mode, no process state)."""
 
     def __init__(self, mode):
         self.on = int(mode)

@@ -93,6 +93,10 @@ class NeRFRenderer(torch.nn.Module):
         # test / benchmark hook: add each pass's sample depths ``z`` (SB, B', K) to the
         # output dicts (fine-pass parity is classified on them, oracle/parity.py)
         self.return_z = False
+        # ray-march schedule of this renderer's fused calls (pnr_render_cfg.march_mode, ABI 3):
+        # None = the library default (pnr_render_set_fused, initially 2), else 0, 1 or 2; all
+        # give bit-identical results; per call, so renderers in different threads may differ
+        self.march_mode = None
 
     # ---- random streams (nerf.py:111, 135, 141, 158) ---------------------------------
     def fine_counts(self):
@@ -299,7 +303,8 @@ class NeRFRenderer(torch.nn.Module):
                                B // sb, kc, kf, kfd, float(self.depth_std), bool(self.white_bkgd),
                                bool(self.lindisp), u_c, u_f, u_j, n_d, int(seed or 0), int(offset),
                                bool(want_weights), bool(self.return_z),
-                               torchops.EVENTS_HOOK(B, kc, kf) if torchops.EVENTS_HOOK else [])
+                               torchops.EVENTS_HOOK(B, kc, kf) if torchops.EVENTS_HOOK else [],
+                               -1 if self.march_mode is None else int(self.march_mode))
         c_rgb, c_depth, c_w, f_rgb, f_depth, f_w, z_c, z_f = res
         outputs = DotMap(coarse=self._pack_out(c_w if want_weights else None, c_rgb, c_depth, sb, want_weights,
                                                z_c if self.return_z else None))

@@ -379,7 +379,36 @@ def test_gen_rays_matches_reference_fixture():
 
 
 # ------------------------------------------------------------------ render --
-def compare_render(name, out, cfg, arr, max_flips=MAX_FLIPS):
+def fixture_oracle(cfg, arr):
+    """(sd, scene, model_kw, white_bkgd, rays_per_obj) of a golden fixture, for the oracle fine
+    pass at a flipped ray's own samples (parity.check_flipped_outputs)."""
+    sd = fixtures.state_dict(cfg)
+    scene = ref_cpu.Scene(fixtures.latent_of(cfg), arr["poses"], fixtures.focal_of(arr), cfg["width"],
+                          cfg["height"], fixtures.c_or_none(arr))
+    kw = dict(d_latent=cfg["d_latent"], n_blocks=cfg.get("n_blocks", 5),
+              combine_layer=cfg.get("combine_layer", 3), has_fine=cfg.get("with_fine", True))
+    B = arr["rays"].reshape(-1, 8).shape[0]
+    return sd, scene, kw, bool(cfg["white_bkgd"]), B // cfg.get("sb", 1)
+
+
+def check_flips(name, out, rays, flip_idx, oracle, u_fine=None):
+    """Every flipped fine ray's HIP rgb / depth / weights against the oracle fine pass at the
+    HIP's own fine samples (nerf.py:284-301 at z_fine_hip): no ray escapes an output check."""
+    if not flip_idx:
+        return None
+    assert oracle is not None, "%s: flipped rays %s and no oracle to check their outputs" % (name, flip_idx)
+    sd, scene, kw, white, rpo = oracle
+    f = out.fine
+    res = parity.check_flipped_outputs(sd, scene, rays, f.z, f.rgb, f.depth, f.weights, flip_idx, rpo, white,
+                                       kw, w_coarse_hip=out.coarse.weights, u_fine=u_fine)
+    print("%s: flipped rays %s, boundary distance %s, max |d| vs the oracle fine pass at their own "
+          "samples %s" % (name, flip_idx, res.get("boundary_distance"), res["max_abs"]))
+    assert res["ok"], "%s: flipped rays %s do not match the oracle fine pass at their own samples: %s" % (
+        name, res["bad_rays"], res)
+    return res
+
+
+def compare_render(name, out, cfg, arr, max_flips=MAX_FLIPS, oracle=None):
     """Coarse pass at full tolerance.  Fine pass classified by cause (oracle/parity.py): a
     ray is excluded only when the importance-sample bins recomputed from the HIP and the
     reference coarse weights differ (a proven searchsorted flip), and its HIP fine samples
@@ -424,7 +453,9 @@ def compare_render(name, out, cfg, arr, max_flips=MAX_FLIPS):
     assert_close(depth[keep], arr["fine_depth"].reshape(B)[keep], name + " fine depth")
     assert_close(w[keep], arr["fine_weights"].reshape(B, -1)[keep], name + " fine weights")
     if cls["flip_idx"]:
-        print("%s: proven bin flips on rays %s" % (name, cls["flip_idx"]))
+        if oracle is None and "seed" in cfg:
+            oracle = fixture_oracle(cfg, arr)
+        check_flips(name, out, arr["rays"], cls["flip_idx"], oracle, arr["u_fine"])
     return len(cls["flip_idx"])
 
 
@@ -487,7 +518,8 @@ def test_render_multiobject_vs_oracle():
     from pnr.renderer import DotMap
 
     out = DotMap(coarse=DotMap(out["coarse"]), fine=DotMap(out["fine"]))
-    compare_render("multiobject", out, dict(n_fine=32, n_fine_depth=16), arr)
+    compare_render("multiobject", out, dict(n_fine=32, n_fine_depth=16), arr,
+                   oracle=(sd, scene, {}, True, bp))
 
 
 def test_simple_output_and_empty_rays():
@@ -614,10 +646,16 @@ def test_frame_render_matches_reference_gen_video():
         full = r(net, arr["rays"].to(DEV).reshape(1, -1, 8), want_weights=True)
     B = cfg["size"] ** 2
     assert torch.equal(full.fine.rgb.reshape(-1, 3).cpu(), frames.reshape(-1, 3))   # same render
+    z_exp = parity.expected_fine_sets(arr["rays"], full.coarse.z, full.coarse.weights, full.coarse.depth,
+                                      streams, 64, 32, 16)
     cls = parity.classify_fine(full.coarse.weights.reshape(B, -1), arr["coarse_weights"].reshape(B, -1),
-                               arr["u_fine"], full.fine.z.reshape(B, -1), arr["z_fine"].reshape(B, -1))
+                               arr["u_fine"], full.fine.z.reshape(B, -1), arr["z_fine"].reshape(B, -1), z_exp)
     assert not bool(cls["unexplained"].any()), torch.nonzero(cls["unexplained"]).reshape(-1).tolist()
+    assert not bool(cls["inconsistent"].any()), torch.nonzero(cls["inconsistent"]).reshape(-1).tolist()
     assert len(cls["flip_idx"]) <= MAX_FLIPS, cls["flip_idx"]
+    scene = ref_cpu.Scene(lat, arr["poses"], arr["focal"], cfg["width"], cfg["height"], None)
+    check_flips("frame32", full, arr["rays"], cls["flip_idx"],
+                (synth.pixelnerf_state(cfg["seed"]), scene, {}, True, B), arr["u_fine"])
     ref = arr["frames"]
     assert frames.shape == ref.shape
     ok = close_mask(frames, ref).reshape(B, 3).all(-1)
@@ -736,7 +774,8 @@ def test_fine_pass_reuses_coarse_outputs_when_mlp_fine_is_none(kfd):
                fine_depth=ref["fine"]["depth"], fine_weights=ref["fine"]["weights"], z_fine=ref["fine"]["z"],
                z_coarse=ref["coarse"]["z"], rays=sc["rays"], u_coarse=streams[0], u_fine=streams[1],
                u_fine_jit=streams[2], n_depth=streams[3])
-    compare_render("reuse kfd=%d" % kfd, outs[0], dict(n_fine=128, n_fine_depth=kfd), arr)
+    compare_render("reuse kfd=%d" % kfd, outs[0], dict(n_fine=128, n_fine_depth=kfd), arr,
+                   oracle=(sd_c, scene, {}, True, 96))
 
 
 @pytest.mark.parametrize("name", ["fw_cfg2", "fw_shipped"])
@@ -824,10 +863,18 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
     rays = rays.to(DEV).reshape(sb, -1, 8)
     outs = []
     for mode in (0, 1, 2):   # separate kernels, full fusion, fused passes + fine-draw kernel
-        with _lib.fused_march(mode), torch.no_grad():
+        r.march_mode = mode  # pnr_render_cfg.march_mode (per call, ABI 3)
+        with torch.no_grad():
             torch.manual_seed(11)
             outs.append(r(net, rays, want_weights=True))
+    # the process default (pnr_render_set_fused) still selects the mode of calls without one
+    r.march_mode = None
+    with _lib.fused_march(0), torch.no_grad():
+        torch.manual_seed(11)
+        dflt = r(net, rays, want_weights=True)
     torch.cuda.synchronize()
+    for p in (("coarse", "fine") if kf > 0 else ("coarse",)):
+        assert torch.equal(dflt[p].rgb, outs[0][p].rgb) and torch.equal(dflt[p].z, outs[0][p].z)
     b = outs[0]
     for mode, a in ((1, outs[1]), (2, outs[2])):
         for p in (("coarse", "fine") if kf > 0 else ("coarse",)):
@@ -840,3 +887,62 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
     a = outs[2]
     w = a.coarse.weights
     assert bool((w >= 0).all()) and float(w.sum(-1).max()) <= 1.0 + 1e-5
+
+
+def test_march_modes_in_two_host_threads():
+    """calls are re-entrant with no mutable globals -- two host threads on one
+    device (the DataParallel replicas of nerf.py:370 call from one thread each) render the
+    same rays concurrently, one with the separate kernels (march_mode 0) and one with the fused
+    march (2), each on its own stream, several times; every result is bit-identical to a
+    single-thread render of the fixture rays in mode 2, and the fixture parity holds."""
+    import threading
+
+    cfg, arr = fixtures.load("fw_cfg2")
+    net = hip_net(cfg, arr)
+    rays = arr["rays"].to(DEV)
+    st = [arr[k].to(DEV).float() for k in ("u_coarse", "u_fine", "u_fine_jit", "n_depth")]
+
+    def make(mode):
+        r = NeRFRenderer(n_coarse=cfg["n_coarse"], n_fine=cfg["n_fine"], n_fine_depth=cfg["n_fine_depth"],
+                         depth_std=cfg["depth_std"], white_bkgd=bool(cfg["white_bkgd"]),
+                         lindisp=bool(cfg["lindisp"]))
+        r.return_z = True
+        r.march_mode = mode
+        return r
+
+    def render(r):
+        r.streams = tuple(st)
+        with torch.no_grad():
+            return r(net, rays, want_weights=True)
+
+    net.hip_mlp(True), net.hip_mlp(False), net.hip_proj(True), net.hip_proj(False)   # packs built once
+    ref = render(make(2))
+    compare_render("fw_cfg2/threads-ref", ref, cfg, arr)
+    torch.cuda.synchronize()
+    results, errors = {}, []
+
+    def worker(mode):
+        try:
+            s = torch.cuda.Stream(DEV)
+            r = make(mode)
+            outs = []
+            with torch.cuda.stream(s):
+                for _ in range(4):
+                    outs.append(render(r))
+            s.synchronize()
+            results[mode] = outs
+        except Exception as e:   # surfaced below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=worker, args=(m,)) for m in (0, 2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert not errors, errors
+    for mode in (0, 2):
+        assert len(results[mode]) == 4
+        for o in results[mode]:
+            for p in ("coarse", "fine"):
+                for k in ("rgb", "depth", "weights", "z"):
+                    assert torch.equal(o[p][k], ref[p][k]), (mode, p, k)

@@ -46,6 +46,7 @@ def setup(n_rays=64, seed=0):
     net.encode_latent(sc["latent"].to(DEV), sc["poses"].to(DEV), sc["focal"].to(DEV), (128, 128))
     scene = ref_cpu.Scene(sc["latent"], sc["poses"], sc["focal"], 128, 128, None)
     model_fn = lambda p, c, d: ref_cpu.pixelnerf_forward(sd, scene, p, c, d)  # noqa: E731
+    model_fn.scene = scene
     return net, sc, model_fn
 
 
@@ -95,6 +96,11 @@ def test_counter_render_equals_injected_replay_and_oracle():
     cls = parity.classify_fine(out.coarse.weights[0], ref["coarse"]["weights"][0], st[1], out.fine.z[0],
                                ref["fine"]["z"], z_exp)
     assert not cls["unexplained"].any() and not cls["inconsistent"].any() and len(cls["flip_idx"]) <= 1
+    if cls["flip_idx"]:   # a flipped ray's outputs against the oracle fine pass at its own samples
+        res = parity.check_flipped_outputs(synth.pixelnerf_state(1), model_fn.scene, sc["rays"], out.fine.z,
+                                           out.fine.rgb, out.fine.depth, out.fine.weights, cls["flip_idx"], 64,
+                                           True, w_coarse_hip=out.coarse.weights, u_fine=st[1])
+        assert res["ok"], res
     keep = ~cls["flip"]
     assert close(out.fine.rgb[0].cpu()[keep], ref["fine"]["rgb"][0][keep])
     assert close(out.fine.depth[0].cpu()[keep], ref["fine"]["depth"][0][keep])

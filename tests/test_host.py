@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.pnr_abi_version() == 2
+    assert lib.pnr_abi_version() == 3
     # an invalid call fails with a message, without touching the GPU
     rc = lib.pnr_composite(None, None, None, 4, 0, 0, None, None, None, None)
     assert rc == -1
@@ -178,7 +178,7 @@ def test_torch_ops_registered_with_meta_shapes():
     lat, cams, pk = torch.empty(1, 32, 32, 512, **m), torch.empty(1, 16, **m), torch.empty(8, **m)
     desc = [42, 512, 512, 4, 5, 3, 12, 3]
     out = ops.render_rays(lat, cams, 1, 1, 64.0, 64.0, desc, pk, pk, None, None, rays, 6, 64, 32, 16, 0.01,
-                          True, False, None, None, None, None, 7, 0, True, True)
+                          True, False, None, None, None, None, 7, 0, True, True, [], 1)
     assert [tuple(t.shape) for t in out] == [(6, 3), (6,), (6, 64), (6, 3), (6,), (6, 96), (6, 64), (6, 96)]
     q = ops.point_query(lat, cams, 1, 1, 64.0, 64.0, desc, pk, None, torch.empty(1, 10, 3, **m), None)
     assert tuple(q.shape) == (1, 10, 4)
@@ -224,6 +224,32 @@ def test_render_set_fused_modes():
         assert lib.pnr_render_set_fused(2) == 2
         with _lib.fused_march(0):
             assert lib.pnr_render_set_fused(0) == 0
+        assert lib.pnr_render_set_fused(2) == 2
+    finally:
+        lib.pnr_render_set_fused(prev)
+
+
+def test_render_cfg_march_mode_is_per_call():
+    """ABI 3: pnr_render_cfg.march_mode names the march schedule of one call; a value outside
+    -1..2 is refused before any device work (host-side validation only: the pointers below
+    are never dereferenced), and the refusal does not touch the process default."""
+    lib = _lib.load()
+    assert ctypes.sizeof(_lib.RenderCfg) == 28
+    buf = ctypes.create_string_buffer(4096 + 16)
+    p = ctypes.c_void_p((ctypes.addressof(buf) + 15) & ~15)   # 16-B aligned, never read
+    sc = _lib.Scene(p, p, 1, 1, 4, 4, 512, 64.0, 64.0)
+    desc = _lib.MlpDesc(42, 512, 512, 4, 5, 3, 12, 3)
+    rays = _lib.Rays(p, 4, 4)
+    rng = _lib.Rng(None, None, None, None, 1, 0)
+    out = _lib.RenderOut(p, p, None, p, p, None, None, None)
+    prev = lib.pnr_render_set_fused(2)
+    try:
+        for bad in (-2, 3, 7):
+            cfg = _lib.RenderCfg(64, 64, 0, 0.01, 1, 0, bad)
+            rc = lib.pnr_render_forward_proj(ctypes.byref(sc), ctypes.byref(desc), p, p, None, None,
+                                             ctypes.byref(rays), ctypes.byref(rng), ctypes.byref(cfg),
+                                             ctypes.byref(out), p, 0, None, None)
+            assert rc == -1 and b"march_mode" in lib.pnr_last_error(), (bad, rc, lib.pnr_last_error())
         assert lib.pnr_render_set_fused(2) == 2
     finally:
         lib.pnr_render_set_fused(prev)

@@ -85,3 +85,48 @@ def test_marginal_draws_may_take_either_neighbouring_bin():
     bad[:, 3] += 1e-2
     cls = parity.classify_fine(w, w, arr["u_fine"], bad, z0, (z0, z1))
     assert bool((cls["inconsistent"] == cls["flip"]).all())
+
+
+def test_marginal_rule_needs_expected_sets():
+    """without z_expected_hip a marginal draw does not excuse differing samples --
+    they are unexplained unless the bins themselves differ."""
+    cfg, arr = fixtures.load("fw_shipped")
+    B = arr["rays"].reshape(-1, 8).shape[0]
+    w = arr["coarse_weights"].reshape(B, -1)
+    streams = (arr["u_coarse"], arr["u_fine"], arr["u_fine_jit"], arr["n_depth"])
+    z0, z1 = parity.expected_fine_sets(arr["rays"], arr["z_coarse"], w, arr["coarse_depth"], streams,
+                                       cfg["n_coarse"], cfg["n_fine"], cfg["n_fine_depth"],
+                                       cfg.get("depth_std", 0.01))
+    moved = (z0 != z1).any(-1)
+    cls = parity.classify_fine(w, w, arr["u_fine"], z1, z0)
+    assert torch.equal(cls["unexplained"], moved) and not cls["flip"].any()
+    cls = parity.classify_fine(w, w, arr["u_fine"], z1, z0, (z0, z1))
+    assert torch.equal(cls["flip"], moved) and not cls["unexplained"].any()
+
+
+def test_flipped_ray_outputs_are_checked_against_the_oracle_fine_pass():
+    """check_flipped_outputs recomputes the oracle fine pass at the given (HIP) fine samples:
+    the fixture's own outputs at the fixture's samples pass, a perturbed rgb or weight fails
+    and names its ray, and multi-object batches are split per object."""
+    from oracle import ref_cpu
+
+    for name in ("rw_ns1", "rw_ns3_sb2"):
+        cfg, arr = fixtures.load(name)
+        sd = fixtures.state_dict(cfg)
+        scene = ref_cpu.Scene(fixtures.latent_of(cfg), arr["poses"], fixtures.focal_of(arr), cfg["width"],
+                              cfg["height"], fixtures.c_or_none(arr))
+        kw = dict(d_latent=cfg["d_latent"], n_blocks=cfg.get("n_blocks", 5),
+                  combine_layer=cfg.get("combine_layer", 3), has_fine=cfg.get("with_fine", True))
+        B = arr["rays"].reshape(-1, 8).shape[0]
+        rpo = B // cfg.get("sb", 1)
+        idx = [0, 3, B - 1]
+        args = (sd, scene, arr["rays"], arr["z_fine"], arr["fine_rgb"], arr["fine_depth"], arr["fine_weights"])
+        res = parity.check_flipped_outputs(*args, idx, rpo, bool(cfg["white_bkgd"]), kw,
+                                           w_coarse_hip=arr["coarse_weights"], u_fine=arr["u_fine"])
+        assert res["ok"], (name, res)
+        assert len(res["boundary_distance"]) == 3
+        rgb = arr["fine_rgb"].clone().reshape(B, 3)
+        rgb[B - 1, 1] += 1e-3
+        res = parity.check_flipped_outputs(sd, scene, arr["rays"], arr["z_fine"], rgb, arr["fine_depth"],
+                                           arr["fine_weights"], idx, rpo, bool(cfg["white_bkgd"]), kw)
+        assert not res["ok"] and res["bad_rays"] == [B - 1], (name, res)
