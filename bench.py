@@ -316,7 +316,7 @@ def cfg2_leg(args, dev, probe):
 
 # ----------------------------------------------------------------- cfg5 --------------
 def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256, ns=1, graph=False,
-              sync_debug=False):
+              sync_debug=False, bn=None):
     """cfg5 (BASELINE configs[4]; the reference's train.py:182-283) on synthetic SRN-shaped
     data: encode SB x NS source images (ResNet34 trunk), render SB x B' rays with the shipped
     conf (64 coarse + 32 fine incl. 16 depth, white background) through the HIP training path
@@ -330,6 +330,10 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
     net = make_model(model_conf()).to(dev)
     net.load_state_dict(synth.pixelnerf_state(0), strict=False)
     net.mlp_precision = precision
+    # encoder BatchNorm over ranks: the reference encodes the whole step's objects in one batch
+    # (train.py:257-262), so at N > 1 the statistics are synchronised over the ranks
+    bn = bn or ("sync" if world > 1 else "batch")
+    pdist.set_batchnorm_mode(net.encoder, bn)
     net.train()
     renderer = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(dev)
     # fused Adam: one multi-tensor kernel per step (the reference uses torch.optim.Adam, same update);
@@ -409,6 +413,8 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
         "config": {"workload": "cfg5: SB=%d objects x %d rays per rank, %d source view(s), 64 coarse + 32 fine "
                                "(16 depth)" % (sb, per, ns), "global_batch_rays": sb * per * world,
                    "parallelism": "data parallel, 1 process per GPU, bucketed RCCL all-reduce (32 MB buckets)",
+                   "encoder_batchnorm": bn + (" (statistics all-reduced over the ranks, pnr.dist.SyncBatchNorm2d)"
+                                              if bn == "sync" else ""),
                    "launch": "one HIP graph per step" if graph else "eager"},
         "loss": round(float(loss.item()), 6),
     }

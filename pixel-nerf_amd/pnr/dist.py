@@ -12,9 +12,12 @@ import os
 
 import torch
 import torch.distributed as dist
+import torch.nn.functional as F
+from torch import nn
 
 __all__ = ["shard_range", "env_rank", "init_from_env", "max_over_ranks", "render_sharded",
-           "gather_to_rank0", "allreduce_grads"]
+           "gather_to_rank0", "allreduce_grads", "SyncBatchNorm2d", "FrozenBatchNorm2d",
+           "set_batchnorm_mode"]
 
 # xGMI is point-to-point (7 links x ~153 GB/s per GPU): RCCL's ring all-reduce is per-link
 # bound, so a few large buckets beat many small ones.  The whole training gradient is
@@ -115,4 +118,118 @@ def allreduce_grads(params, world, bucket_bytes=BUCKET_BYTES):
             g.copy_(flat[o: o + g.numel()].view_as(g))
             o += g.numel()
         n += 1
+    return n
+
+
+# ---- encoder BatchNorm across ranks (SURVEY §8(e) "semantics difference to resolve") ------
+# The reference encodes all SB objects of a step in ONE batch on device 0 (train.py:257-262)
+# with the ResNet34's BatchNorm in train mode (encoder.py:28-53, trainer.py:194), so the
+# statistics are over the whole SB x NS image batch.  One process per GPU with each rank
+# encoding its own objects would normalise over that rank's share only, and the running
+# statistics would drift apart between ranks.  SyncBatchNorm2d restores the reference's
+# semantics: the per-channel sums of the batch are all-reduced (one collective per layer in
+# the forward, one in the backward), so every rank normalises with the full batch's mean and
+# biased variance and updates identical running statistics (unbiased variance, as torch's
+# BatchNorm does).  FrozenBatchNorm2d is the other resolution SURVEY §8(e) names: the
+# running statistics are used and never updated (eval-mode BN, what the reference's step 0
+# runs because render_par is built .eval(), train.py:93).
+
+
+class _SyncBNFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, group):
+        C = x.shape[1]
+        dims = [0] + list(range(2, x.dim()))
+        xd = x.double()
+        n_local = x.numel() // C
+        stats = torch.cat([xd.sum(dims), (xd * xd).sum(dims),
+                           torch.full((1,), float(n_local), dtype=torch.float64, device=x.device)])
+        dev_cpu = dist.get_backend(group) != "nccl" and x.device.type != "cpu"
+        red = stats.cpu() if dev_cpu else stats   # gloo reduces host tensors
+        dist.all_reduce(red, group=group)
+        stats = red.to(x.device) if dev_cpu else red
+        n = stats[-1]
+        mean = stats[:C] / n
+        var = (stats[C:2 * C] / n - mean * mean).clamp_min(0.0)   # biased, as BatchNorm normalises
+        invstd = torch.rsqrt(var + eps)
+        if running_mean is not None:
+            with torch.no_grad():
+                running_mean.mul_(1.0 - momentum).add_(mean.to(running_mean.dtype), alpha=momentum)
+                # on the device: no host read of the count (a sync per layer)
+                unbiased = torch.where(n > 1, var * n / (n - 1.0).clamp_min(1.0), var)
+                running_var.mul_(1.0 - momentum).add_(unbiased.to(running_var.dtype), alpha=momentum)
+        shape = [1, C] + [1] * (x.dim() - 2)
+        mean_f = mean.to(x.dtype).view(shape)
+        invstd_f = invstd.to(x.dtype).view(shape)
+        xhat = (x - mean_f) * invstd_f
+        ctx.save_for_backward(xhat, invstd_f, weight, n.reshape(1))
+        ctx.group = group
+        ctx.dev_cpu = dev_cpu
+        return xhat * weight.view(shape) + bias.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xhat, invstd, weight, n = ctx.saved_tensors
+        C = xhat.shape[1]
+        dims = [0] + list(range(2, xhat.dim()))
+        shape = [1, C] + [1] * (xhat.dim() - 2)
+        dy = dy.contiguous()
+        sum_dy = dy.sum(dims)
+        sum_dy_xhat = (dy * xhat).sum(dims)
+        red = torch.cat([sum_dy, sum_dy_xhat]).double()
+        red = red.cpu() if ctx.dev_cpu else red
+        dist.all_reduce(red, group=ctx.group)
+        red = red.to(dy.device) / n
+        mean_dy = red[:C].to(dy.dtype).view(shape)
+        mean_dy_xhat = red[C:].to(dy.dtype).view(shape)
+        dx = (dy - mean_dy - xhat * mean_dy_xhat) * (invstd * weight.view(shape))
+        # the affine parameters' gradients stay local: the data-parallel gradient mean
+        # (allreduce_grads) sums them over ranks like every other parameter's
+        return dx, sum_dy_xhat, sum_dy, None, None, None, None, None
+
+
+class SyncBatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d whose train-mode statistics span every rank of ``group`` (the
+    reference's single-process batch, train.py:257-262).  Same parameters, buffers and
+    state-dict keys as BatchNorm2d; eval mode and a one-rank world are plain BatchNorm2d."""
+
+    group = None
+
+    def forward(self, x):
+        world = dist.get_world_size(self.group) if dist.is_available() and dist.is_initialized() else 1
+        if not self.training or world == 1:
+            return super().forward(x)
+        if not self.affine or not self.track_running_stats or self.momentum is None:
+            raise NotImplementedError("SyncBatchNorm2d: affine, tracked stats and a float momentum only")
+        self.num_batches_tracked.add_(1)
+        return _SyncBNFunction.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
+                                     self.eps, self.momentum, self.group)
+
+
+class FrozenBatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d that always normalises with its running statistics and never updates
+    them (eval-mode BN inside a training step).  Same parameters and state-dict keys; the
+    affine weight and bias still train."""
+
+    def forward(self, x):
+        return F.batch_norm(x, self.running_mean, self.running_var, self.weight, self.bias, False, 0.0, self.eps)
+
+
+_BN_CLASSES = {"batch": nn.BatchNorm2d, "sync": SyncBatchNorm2d, "frozen": FrozenBatchNorm2d}
+
+
+def set_batchnorm_mode(module, mode, group=None):
+    """Switch every BatchNorm2d of ``module`` (e.g. a PixelNeRFNet's encoder) in place to
+    ``mode``: "batch" (the reference: statistics of this process's batch), "sync" (statistics
+    of the whole batch over the ranks of ``group``: the reference's semantics under one process
+    per GPU), or "frozen" (running statistics, never updated).  Parameters, buffers and
+    state-dict keys are unchanged.  Returns the number of layers switched."""
+    cls = _BN_CLASSES[mode]
+    n = 0
+    for m in module.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m.__class__ = cls
+            if cls is SyncBatchNorm2d:
+                m.group = group
+            n += 1
     return n

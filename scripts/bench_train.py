@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--rays-per-obj", type=int, default=256)
     ap.add_argument("--precision", default="f16x3")
     ap.add_argument("--views", type=int, default=1, help="source views per object (train.py -V)")
+    ap.add_argument("--bn", choices=["batch", "sync", "frozen"], default=None,
+                    help="encoder BatchNorm: batch (per process), sync (over the ranks; default at N > 1), frozen")
     ap.add_argument("--graph", action="store_true",
                     help="replay the step captured as one HIP graph (measured within 1 %% of eager)")
     ap.add_argument("--sync-debug", action="store_true",

@@ -164,3 +164,102 @@ def test_two_rank_gloo_gradient_allreduce_equals_full_batch():
     assert n_coll >= 2   # several buckets
     for k, p in ref.items():
         torch.testing.assert_close(torch.from_numpy(got[k]), p.grad, atol=1e-6, rtol=1e-4, msg=k)
+
+
+# ---- encoder BatchNorm across ranks (train.py:257-262, encoder.py:28-53) -----
+def _encoder_step(images, weights, mode, world=1):
+    """One training-mode encoder pass of `images` (n, 3, H, W) through the ResNet34 trunk +
+    latent concat (pnr.encoder.SpatialEncoder), loss = mean over ranks of
+    sum(latent * weights): returns (latent, grads by name, running stats by name)."""
+    from pnr.encoder import SpatialEncoder
+
+    torch.manual_seed(0)
+    enc = SpatialEncoder(pretrained=False, use_first_pool=False).double()
+    pdist.set_batchnorm_mode(enc, mode)
+    enc.train()
+    enc.latent = torch.empty(1, 1, 1, 1, dtype=torch.float64)
+    lat = enc(images)
+    loss = (lat * weights).sum()
+    loss.backward()
+    params = [p for _, p in enc.named_parameters()]
+    pdist.allreduce_grads(params, world)
+    grads = {k: p.grad.clone() for k, p in enc.named_parameters() if p.grad is not None}
+    stats = {k: v.clone() for k, v in enc.state_dict().items() if "running" in k or "num_batches" in k}
+    return lat.detach(), grads, stats
+
+
+def _bn_inputs():
+    g = torch.Generator().manual_seed(7)
+    images = torch.rand(4, 3, 32, 32, generator=g, dtype=torch.float64) * 2 - 1
+    weights = torch.randn(4, 512, 16, 16, generator=g, dtype=torch.float64)
+    return images, weights
+
+
+def _bn_worker(rank, world, port, mode, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    r, w, _ = pdist.init_from_env("gloo")
+    images, weights = _bn_inputs()
+    s, e = pdist.shard_range(images.shape[0], r, w)
+    # rank r's loss is its share of the full-batch loss x world (mean over ranks = full loss)
+    lat, grads, stats = _encoder_step(images[s:e], weights[s:e] * w, mode, w)
+    q.put((r, lat.numpy(), {k: v.numpy() for k, v in grads.items()}, {k: v.numpy() for k, v in stats.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run_bn(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (lat, g, st)) for r, lat, g, st in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return got
+
+
+def test_two_rank_sync_batchnorm_encode_equals_one_rank_full_batch():
+    """SyncBatchNorm2d: a 2-rank train-mode encode of split objects (2 images per rank) equals
+    the 1-rank encode of all 4 (the reference's one-batch encode): latents, every encoder
+    gradient after the data-parallel mean, and both ranks' running statistics."""
+    images, weights = _bn_inputs()
+    ref_lat, ref_g, ref_st = _encoder_step(images, weights, "batch")
+    got = _run_bn("sync")
+    lat = torch.cat([torch.from_numpy(got[r][0]) for r in (0, 1)])
+    torch.testing.assert_close(lat, ref_lat, atol=1e-9, rtol=1e-9)
+    for r in (0, 1):
+        for k, v in ref_g.items():
+            # fp64 sums over a different association (per-rank partial sums, sum / sum-of-squares
+            # variance) through ~30 normalised layers: agreement to ~1e-7 of the gradient's scale
+            torch.testing.assert_close(torch.from_numpy(got[r][1][k]), v, atol=1e-7 * float(v.abs().max()),
+                                       rtol=1e-6, msg=k)
+        for k, v in ref_st.items():
+            torch.testing.assert_close(torch.from_numpy(got[r][2][k]), v, atol=1e-9, rtol=1e-9, msg=k)
+
+
+def test_two_rank_local_batchnorm_differs_and_frozen_matches_eval():
+    """Without the sync each rank normalises over its own share (the semantic gap SURVEY §8(e)
+    names): its latent differs from the full-batch encode.  FrozenBatchNorm2d uses the running
+    statistics, so its train-mode encode equals an eval-mode encode and leaves them untouched."""
+    from pnr.encoder import SpatialEncoder
+
+    images, weights = _bn_inputs()
+    ref_lat, _, _ = _encoder_step(images, weights, "batch")
+    got = _run_bn("batch")
+    lat = torch.cat([torch.from_numpy(got[r][0]) for r in (0, 1)])
+    assert float((lat - ref_lat).abs().max()) > 1e-3
+    lat_f, _, st_f = _encoder_step(images, weights, "frozen")
+    torch.manual_seed(0)
+    enc = SpatialEncoder(pretrained=False, use_first_pool=False).double().eval()
+    enc.latent = torch.empty(1, 1, 1, 1, dtype=torch.float64)
+    with torch.no_grad():
+        ev = enc(images)
+    torch.testing.assert_close(lat_f, ev, atol=1e-12, rtol=1e-12)
+    for k, v in st_f.items():
+        if "running_mean" in k:
+            assert float(v.abs().max()) == 0.0, k

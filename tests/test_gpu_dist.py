@@ -44,11 +44,12 @@ def test_bench_gpus_2_launches_its_own_ranks():
     """`python bench.py --gpus 2` -- the form the driver's scaling runs use -- starts its own 2
     ranks (torch.distributed.run as a child; both on device 0 with gloo here, one per GPU with
     RCCL on a node) and reports the whole batch over both ranks: n_gpus 2, rank 0's shard is half
-    of the 98,304-ray cfg3 batch."""
+    of the 98,304-ray cfg3 batch.  The cfg5 train leg runs with the encoder's BatchNorm
+    synchronised over the 2 ranks (pnr.dist.SyncBatchNorm2d on HIP tensors)."""
     env = dict(os.environ, PNR_DIST_BACKEND="gloo", PNR_FORCE_DEVICE="0", OMP_NUM_THREADS="4")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--no-train"]
+           "--warmup", "1", "--train-steps", "2"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -56,3 +57,6 @@ def test_bench_gpus_2_launches_its_own_ranks():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["rays_rank0"] == 49152 and res["value"] > 0
     assert res["config"]["rays_per_step"] == 98304
+    tr = res["train"]
+    assert tr["n_gpus"] == 2 and tr["config"]["encoder_batchnorm"].startswith("sync") and tr["value"] > 0
+    assert tr["loss"] == tr["loss"]   # finite
