@@ -377,8 +377,7 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
-            *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) =
-                f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+            *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = relu4(v);
         }
     }
 }
@@ -740,15 +739,19 @@ __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wav
     const int g = lane >> 4, cl = lane & 15;
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
-        float m = 0.f;
+        float m = 0.f;   // max(0, ...) = the max of the relu'd values
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             f4 v = acc[r][c];
             if constexpr (!RELU) v = f4{fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
-            m = fmaxf(m, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
+            m = max3_nc(max3_nc(m, v.x, v.y), v.z, v.w);
         }
+#ifdef PNR_SHFL_COLMAX
         m = fmaxf(m, __shfl_xor(m, 16, 64));
         m = fmaxf(m, __shfl_xor(m, 32, 64));
+#else
+        m = rows_max(m);
+#endif
         if (g == 0) {
             cmax[(16 * c + cl) * 8 + wave] = m;
             if constexpr (WAVES == 4) cmax[(16 * c + cl) * 8 + wave + 4] = m;
@@ -768,14 +771,13 @@ __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _
         const int col = 16 * c + cl;
         const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
         const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
-        const int e = scale_exp(fmaxf(fmaxf(fmaxf(m0.x, m0.y), fmaxf(m0.z, m0.w)),
-                                      fmaxf(fmaxf(m1.x, m1.y), fmaxf(m1.z, m1.w))));
+        const int e = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
         const float sc = __builtin_ldexpf(1.f, e);
         if (wave == 0 && g == 0) ecol[col] = e;
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
-            const f4 o = RELU ? f4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)} : v;
+            const f4 o = RELU ? relu4(v) : v;
             put_split4(P0, P1, col * ROWH + swz(col, 16 * (RTW * wave + r) + 4 * g), o, sc);
         }
     }

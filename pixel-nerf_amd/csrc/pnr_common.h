@@ -92,6 +92,21 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
+// IEEE-754-2019 maximum (v_maximum3_f32 on gfx950: NaN-propagating like torch.relu / torch.max,
+// so no operand canonicalization; fmaxf's quieting doubled the max count of every publish)
+__device__ __forceinline__ float max_nc(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float max3_nc(float a, float b, float c) { return max_nc(max_nc(a, b), c); }
+__device__ __forceinline__ f4 relu4(const f4 &v) { return __builtin_elementwise_maximum(v, f4{0.f, 0.f, 0.f, 0.f}); }
+// max over the four 16-lane rows of the wave, every lane: v_permlane16_swap / v_permlane32_swap
+// of a value with itself puts the row partner's value in one of the two results (max is symmetric,
+// so which one does not matter); VALU only, no LDS crossbar round trip
+__device__ __forceinline__ float rows_max(float m) {
+    const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    m = max_nc(__uint_as_float(r16[0]), __uint_as_float(r16[1]));
+    const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    return max_nc(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
+}
+
 // ---- counter-based random streams (pnr_rng {seed, offset}, include/pnr_abi.h) ----------
 // Philox4x32-10 (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1, 2, 3",
 // SC'11; the Random123 constants).  Draw e of stream s keyed by `seed` uses the counter
