@@ -812,6 +812,9 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
     }
 }
 
+#ifndef PNR_LOCKSTEP
+#define PNR_LOCKSTEP 0
+#endif
 #ifndef PNR_PARK_X
 #define PNR_PARK_X 0
 #endif
@@ -1266,8 +1269,21 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     float *mscr = mreg + MARCH_BUF_FLOATS;
     float *mnf = mscr + 384;
     const int kpt = MARCH ? march_cfg(a)->kpt : 1;   // tiles per scheduling unit (a ray when marching)
+    // PNR_LOCKSTEP = E > 0 (diagnostic A/B): static per-XCD rounds instead --
+    // workgroup j of XCD x takes unit lo_x + r n_x + j in round r -- and every E rounds the
+    // XCD's workgroups meet at a spin barrier, so that they run the same layers at the same time
+    // and one layer's weight fragments serve all 32 CUs from the XCD's 4 MB L2.  The barrier is
+    // pacing only (no data crosses it): the spin is bounded (50 us) and a timed-out wait proceeds.
+    int lk_round = 0;   // tid 0: rounds taken
     auto grab = [&]() -> int {
         const int64_t T = a.n_tiles >> (kpt - 1);   // kpt is 1 or 2
+        if constexpr (PNR_LOCKSTEP > 0) {
+            const int x = blockIdx.x & 7, nx = ((int)gridDim.x - x + 7) >> 3, j = blockIdx.x >> 3;
+            const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
+            const int64_t i = lo + (int64_t)lk_round * nx + j;
+            s_next[1] = lk_round++;
+            return i < hi ? (int)(i << (kpt - 1)) : (int)a.n_tiles;
+        }
         const int x0 = blockIdx.x & 7;
         for (int k = 0; k < 8; ++k) {
             const int x = (x0 + k) & 7;
@@ -1281,6 +1297,25 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     if (tid == 0) *s_next = grab();
     lds_barrier();
     for (int64_t tile = *s_next; tile < a.n_tiles; tile = *s_next) {
+        if constexpr (PNR_LOCKSTEP > 0) {
+            const int rnd = s_next[1];   // written with s_next, read after the same barrier
+            if ((tile & (kpt - 1)) == 0 && rnd > 0 && rnd % PNR_LOCKSTEP == 0) {
+                if (tid == 0) {
+                    const int x = blockIdx.x & 7, nx = ((int)gridDim.x - x + 7) >> 3;
+                    const int64_t T = a.n_tiles >> (kpt - 1), lo = x * T / 8, hi = (x + 1) * T / 8;
+                    const int64_t left = hi - lo - (int64_t)rnd * nx;   // units of this round
+                    const int part = left < nx ? (int)left : nx;
+                    const int target = (rnd / PNR_LOCKSTEP - 1) * nx + part;
+                    int *cnt = a.tile_ctr + 16 * x;
+                    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+                    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+                           __builtin_amdgcn_s_memrealtime() - t0 < 5000)   // 100 MHz: 50 us
+                        __builtin_amdgcn_s_sleep(2);
+                }
+                lds_barrier();
+            }
+        }
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         // (addresses formed at use: nothing per tile stays live across the GEMMs)
         auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + opaque_lane(lane) * 4; };
