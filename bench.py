@@ -91,6 +91,7 @@ RAY_BATCH = 50000              # gen_video.py --ray_batch_size default (args.py:
 CHUNK = 4096
 W = H = 128
 FUSED_MARCH = True   # pnr_render_set_fused(2) (main: --unfused / --fused-mode)
+MARCH_MODE = 2       # the fused mode (3: both passes in one launch)
 KERNELS = ["sample_coarse", "mlp_coarse", "composite_coarse", "sample_fine", "mlp_fine", "composite_fine"]
 
 
@@ -156,22 +157,26 @@ class RenderProbe:
         """Per-kernel mean ms, and the fine MLP's roofline over the recorded launches."""
         per = {n: [] for n in KERNELS}
         pts = []
+        single = False
         for evs, n, kc, kf in self.calls:
             for i, name in enumerate(KERNELS):
                 per[name].append(self.ev.elapsed_ms(evs[i], evs[i + 1]))
-            pts.append(n * (kc + kf))
+            # march mode 3 runs both passes in the launch events [1]-[2] time
+            single = FUSED_MARCH and MARCH_MODE == 3 and latent_proj and kc == 64 and kc + kf == 128
+            pts.append(n * (kc + kc + kf) if single else n * (kc + kf))
         avg = {k: sum(v) / len(v) for k, v in per.items() if v}
         kflop = KERNEL_FLOP_PER_POINT_NS1 if latent_proj else FLOP_PER_POINT_NS1
         pts_per_launch = sum(pts) / len(pts)
         flop = pts_per_launch * kflop
-        ms = avg["mlp_fine"]
+        ms = avg["mlp_coarse"] if single else avg["mlp_fine"]
         achieved = flop / (ms * 1e-3) / 1e12
         peak, terms = PEAK_BY_PRECISION[precision]
         # the fine pass (K = 128) runs the fused-march instantiation unless --unfused
         kname = "k_point_mlp<%d, %s, %s>" % (PRECISIONS[precision], "true" if latent_proj else "false",
                                              "true" if FUSED_MARCH else "false")
         return avg, {
-            "kernel": "k_point_mlp (fine pass)", "bound": "mfma",
+            "kernel": "k_point_mlp (single-launch march: coarse + fine pass)" if single else "k_point_mlp (fine pass)",
+            "bound": "mfma",
             "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s (fp32-equivalent: algorithmic FLOP per launch (%d FLOP per point x points "
                     "per launch) / mean launch duration, HIP events on the launch stream)" % kflop,
@@ -758,15 +763,16 @@ def main():
                     help="separate sample / MLP / composite kernels instead of the fused ray march (A/B)")
     ap.add_argument("--fused-mode", type=int, default=2,
                     help="pnr_render_set_fused: 2 fused passes + fine-draw kernel (default), 1 fine draws "
-                         "in the coarse epilogue too")
+                         "in the coarse epilogue too, 3 both passes in one launch")
     args = ap.parse_args()
     # `python bench.py --gpus N` (N > 1) outside torch.distributed.run: launch the N ranks as
     # a child before anything here touches the GPU, and exit with their status
     if check_world(args.gpus):
         sys.stdout.flush()
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
-    global FUSED_MARCH
+    global FUSED_MARCH, MARCH_MODE
     FUSED_MARCH = not args.unfused
+    MARCH_MODE = 0 if args.unfused else args.fused_mode
     if hasattr(_lib.load(), "pnr_render_set_fused"):   # absent only in A/B builds of older revisions
         _lib.load().pnr_render_set_fused(0 if args.unfused else args.fused_mode)
 
@@ -796,6 +802,10 @@ def main():
         "dtype": "f32",
         "arithmetic": ARITHMETIC[args.precision],
         "march": ("separate sample / MLP / composite kernels" if args.unfused else
+                  "fused (mode 3): ONE k_point_mlp launch per batch -- a ray's coarse tile (coarse draws in "
+                  "its prologue, composite + fine draws in its epilogue, fine depths kept in LDS), then its two "
+                  "fine tiles (composite in the epilogue); roofline.launch_ms is that launch"
+                  if args.fused_mode == 3 else
                   "fused (mode %d): one k_point_mlp launch per pass, coarse draws in its prologue, the "
                   "composite in its epilogue (roofline.launch_ms includes them); fine draws %s"
                   % (args.fused_mode, "in the coarse epilogue" if args.fused_mode == 1 else "in their own kernel")),

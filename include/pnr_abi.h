@@ -134,6 +134,8 @@ typedef struct pnr_render_cfg {
     int32_t white_bkgd;   /*                              (nerf.py:83)       */
     int32_t lindisp;      /*                              (nerf.py:84)       */
     /* ABI 3: ray-march schedule of THIS call (no process state is read or written):
+     *   3  coarse and fine pass in ONE launch (n_coarse = 64, n_coarse + n_fine = 128,
+     *      projected latents; other shapes run mode 2),
      *   2  fused passes + fine-draw kernel, 1  fine draws in the coarse epilogue too,
      *   0  separate sample / MLP / composite kernels (see pnr_render_set_fused);
      *  -1  the process default set by pnr_render_set_fused (initially 2).
@@ -196,7 +198,7 @@ int pnr_render_forward(const pnr_scene *scene, const pnr_mlp_desc *desc,
  * no host synchronization is added.  Used by bench.py for per-kernel timing.
  * With the fused ray march (pnr_render_set_fused) a pass is one launch: [1]-[2] and
  * [4]-[5] then time the whole coarse / fine pass (sampling and composite included),
- * and the other intervals are empty. */
+ * and the other intervals are empty; with march_mode 3 the single launch is [1]-[2]. */
 int pnr_render_forward_events(const pnr_scene *scene, const pnr_mlp_desc *desc,
                               const void *coarse_packed, const void *fine_packed,
                               const pnr_rays *rays, const pnr_rng *rng,
@@ -238,7 +240,13 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc,
                             void *workspace, size_t workspace_bytes, pnr_stream_t stream,
                             void *const *events);
 
-/* Fused ray march.  2 (the default): each pass of pnr_render_forward* is one k_point_mlp launch
+/* Fused ray march.  3: the whole march is ONE k_point_mlp launch -- a workgroup takes a ray's
+ * coarse tile, composites it and draws its fine samples in the epilogue into LDS, then runs the
+ * ray's two fine tiles with the fine MLP and composites them (nerf.py:273-301 per ray; the fine
+ * depths never reach HBM unless pnr_render_out.z_fine asks for them).  It applies to
+ * n_coarse = 64, n_coarse + n_fine = 128 with both projected latents (the headline shape) and
+ * falls back to mode 2 otherwise.  2 (the default): each pass of pnr_render_forward* is one
+ * k_point_mlp launch
  * that draws the coarse depths in its prologue and composites each ray from LDS in its
  * epilogue (the per-point rgb/sigma never reach HBM); the fine draws (inverse CDF + sort) run
  * in their own small kernel between the passes.  1: the coarse epilogue draws the fine samples

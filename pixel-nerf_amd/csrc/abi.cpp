@@ -350,8 +350,8 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     if (!coarse_packed) return fail(PNR_ERR_INVALID, "coarse_packed is NULL");
     const int kc = cfg->n_coarse, kf = cfg->n_fine, kfd = cfg->n_fine_depth;
     if (kc < 1) return fail(PNR_ERR_INVALID, "n_coarse < 1");
-    if (cfg->march_mode < -1 || cfg->march_mode > 2)
-        return fail(PNR_ERR_INVALID, "march_mode must be -1 (default), 0, 1 or 2 (got %d)", cfg->march_mode);
+    if (cfg->march_mode < -1 || cfg->march_mode > 3)
+        return fail(PNR_ERR_INVALID, "march_mode must be -1 (default), 0, 1, 2 or 3 (got %d)", cfg->march_mode);
     const int mode = cfg->march_mode >= 0 ? cfg->march_mode : g_fused_default.load(std::memory_order_relaxed);
     if (kf < 0 || kfd < 0 || kfd > kf) return fail(PNR_ERR_INVALID, "need 0 <= n_fine_depth <= n_fine");
     if (kc + kf > 1024) return fail(PNR_ERR_UNSUPPORTED, "n_coarse + n_fine must be <= 1024");
@@ -408,6 +408,44 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
                         kc <= 64 && sort_width(kall) <= 128;
     const bool fuse_f = fused && kf > 0 && !reuse && kall % 64 == 0 && kall <= 128;
     float *zf = kf > 0 ? (out->z_fine ? out->z_fine : reinterpret_cast<float *>(ws + w.z_f)) : nullptr;
+    // mode 3: both passes in ONE launch (a ray's coarse tile, then its fine tiles; the fine depths
+    // stay in LDS), for kc = 64 and kc + kf = 128 with both projections; other shapes run mode 2
+    const bool single = mode == 3 && fuse_c && kf > 0 && !reuse && kc == 64 && kall == 128 &&
+                        sort_width(kall) <= 128 && coarse_proj && fine_proj;
+    if (single) {
+        MarchCfg m = {};
+        m.kpt = 1;
+        m.sample_coarse = 1;
+        m.lindisp = cfg->lindisp;
+        m.white_bkgd = cfg->white_bkgd;
+        m.u_coarse = r_uc;
+        m.z_out = out->z_coarse;
+        m.weights = out->coarse_weights;
+        m.rgb = out->coarse_rgb;
+        m.depth = out->coarse_depth;
+        m.kf = kf;
+        m.kfd = kfd;
+        m.n_sort = sort_width(kall);
+        m.depth_std = cfg->depth_std;
+        m.u_fine = r_uf;
+        m.u_jit = r_uj;
+        m.n_depth = r_nd;
+        m.z_fine = out->z_fine;   // NULL unless the caller wants the fine depths
+        m.single = 1;
+        m.kpt_f = kall / 64;
+        m.packed_f = static_cast<const float *>(fine_packed);
+        m.proj_f = fine_proj;
+        m.weights_f = out->fine_weights;
+        m.rgb_f = out->fine_rgb;
+        m.depth_f = out->fine_depth;
+        if ((rc = mark(0)) || (rc = mark(1))) return rc;
+        if ((rc = launch_point_mlp(*scene, *desc, coarse_packed, rays->rays, zc, kc, rays->rays_per_obj, nullptr,
+                                   nullptr, 1, n * (kc + kall), nullptr, xsum, st, nullptr, coarse_proj, &m)))
+            return rc;
+        for (int i = 2; i <= 6; ++i)
+            if ((rc = mark(i))) return rc;
+        return PNR_OK;
+    }
 
     // coarse pass (nerf.py:273-276)
     if ((rc = mark(0))) return rc;
@@ -488,7 +526,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     return mark(6);
 }
 
-int32_t pnr_render_set_fused(int32_t on) { return g_fused_default.exchange(on < 0 || on > 2 ? 2 : on); }
+int32_t pnr_render_set_fused(int32_t on) { return g_fused_default.exchange(on < 0 || on > 3 ? 2 : on); }
 
 int pnr_sample_coarse(const float *rays, int64_t n_rays, int32_t n_coarse, const float *u_coarse,
                       int32_t lindisp, float *z, pnr_stream_t stream) {

@@ -189,7 +189,8 @@ __device__ __forceinline__ void sample_fine_wave(int lane, int64_t b, float near
                                                  float depth_std, const RngSrc &u_fine, const RngSrc &u_jit,
                                                  const RngSrc &n_depth, bool lindisp, int n_sort, float *cdf,
                                                  float *s, int *si, float *z_fine, int *origin, float *z_new,
-                                                 bool use_pre = false, FineDraws pre = {0.f, 0.f, 0.f}) {
+                                                 bool use_pre = false, FineDraws pre = {0.f, 0.f, 0.f},
+                                                 float *z_lds = nullptr) {
     EPI_DECL
     // pdf = (w + 1e-5) / sum(w + 1e-5)   (nerf.py:130-131)
     float part = 0.0f;
@@ -245,12 +246,21 @@ __device__ __forceinline__ void sample_fine_wave(int lane, int64_t b, float near
             float v[1] = {s[lane < n_sort ? lane : 0]};
             if (lane >= n_sort) v[0] = __builtin_inff();
             sort_lanes<1>(v, lane);
-            if (lane < k_all) z_fine[b * k_all + lane] = v[0];
+            if (lane < k_all) {
+                if (z_fine) z_fine[b * k_all + lane] = v[0];
+                if (z_lds) z_lds[lane] = v[0];
+            }
         } else {
             float v[2] = {s[lane], s[64 + lane]};
             sort_lanes<2>(v, lane);
-            z_fine[b * k_all + lane] = v[0];
-            if (64 + lane < k_all) z_fine[b * k_all + 64 + lane] = v[1];
+            if (z_fine) {
+                z_fine[b * k_all + lane] = v[0];
+                if (64 + lane < k_all) z_fine[b * k_all + 64 + lane] = v[1];
+            }
+            if (z_lds) {
+                z_lds[lane] = v[0];
+                if (64 + lane < k_all) z_lds[64 + lane] = v[1];
+            }
         }
         EPI_T(3);
         return;
@@ -270,7 +280,10 @@ __device__ __forceinline__ void sample_fine_wave(int lane, int64_t b, float near
             wave_lds_sync();
         }
     }
-    for (int k = lane; k < k_all; k += 64) z_fine[b * k_all + k] = s[k];
+    for (int k = lane; k < k_all; k += 64) {
+        if (z_fine) z_fine[b * k_all + k] = s[k];
+        if (z_lds) z_lds[k] = s[k];
+    }
     if (origin)
         for (int k = lane; k < k_all; k += 64) origin[b * k_all + k] = si[k];
 }
@@ -289,7 +302,13 @@ struct MarchCfg {
     int kf, kfd, n_sort;
     float depth_std;
     RngSrc u_fine, u_jit, n_depth;
-    float *z_fine;               // (n_rays, kc + kf), sorted
+    float *z_fine;               // (n_rays, kc + kf), sorted (may be NULL with `single`)
+    // single-launch march (pnr march_mode 3): the ray's fine pass follows its coarse pass in the
+    // same launch -- a scheduling unit is the ray's kpt coarse tiles, then its kpt_f fine tiles;
+    // the coarse epilogue leaves the sorted fine depths in LDS for them
+    int single, kpt_f;
+    const float *packed_f, *proj_f;          // the fine MLP's pack and projected latent
+    float *weights_f, *rgb_f, *depth_f;      // fine composite outputs (weights_f may be NULL)
 };
 // LDS floats of the fused march region (k_point_mlp): the ray's z (128) | raw (128 x 4), the
 // epilogue scratch w (128) | cdf (128) | sort (128), near / far (4)

@@ -1116,10 +1116,10 @@ __device__ __forceinline__ RngSrc ld_rng(const __attribute__((address_space(4)))
 // composite's.
 template <int S>
 __device__ __forceinline__ void march_ray(const Args &a, int64_t b, const float *buf, const float *nf, float *scr,
-                                          int lane) {
+                                          int lane, bool fine_pass) {
     const CfgPtr c = march_cfg(a);
     EPI_DECL
-    const int kf = c->kf;
+    const int kf = fine_pass ? 0 : c->kf;   // the single-launch fine pass draws nothing
     FineDraws d = {0.f, 0.f, 0.f};
     if (kf > 0) d = fine_draws(lane, b, kf, c->kfd, ld_rng(c->u_fine), ld_rng(c->u_jit), ld_rng(c->n_depth));
     const float near = nf[0], far = nf[1];
@@ -1130,7 +1130,9 @@ __device__ __forceinline__ void march_ray(const Args &a, int64_t b, const float 
         zk[i] = buf[S * lane + i];
         v[i] = *reinterpret_cast<const f4 *>(buf + 128 + 4 * (S * lane + i));
     }
-    const float depth = composite_wave<S>(lane, b, a.K, far, zk, v, c->white_bkgd, c->weights, c->rgb, c->depth, wk);
+    const float depth = fine_pass
+        ? composite_wave<S>(lane, b, COLS * S, far, zk, v, c->white_bkgd, c->weights_f, c->rgb_f, c->depth_f, wk)
+        : composite_wave<S>(lane, b, COLS * S, far, zk, v, c->white_bkgd, c->weights, c->rgb, c->depth, wk);
     EPI_T(0);
 #ifdef PNR_EPI_TIMING
     if (lane == 0) atomicAdd(&g_epi[7], 1ull);
@@ -1140,15 +1142,17 @@ __device__ __forceinline__ void march_ray(const Args &a, int64_t b, const float 
 #pragma unroll
         for (int i = 0; i < S; ++i) w[S * lane + i] = wk[i];
         wave_lds_sync();
-        sample_fine_wave(lane, b, near, far, a.K, w, buf, depth, kf, c->kfd, c->depth_std, RngSrc{}, RngSrc{},
+        // single launch: the sorted fine depths also go to buf's z region (whose coarse depths
+        // composite_wave and the sort's inputs have consumed) for the ray's fine tiles
+        sample_fine_wave(lane, b, near, far, COLS * S, w, buf, depth, kf, c->kfd, c->depth_std, RngSrc{}, RngSrc{},
                          RngSrc{}, c->lindisp != 0, c->n_sort, scr + 128, scr + 256, nullptr, c->z_fine, nullptr,
-                         nullptr, true, d);
+                         nullptr, true, d, c->single ? const_cast<float *>(buf) : nullptr);
     }
 }
 __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const float *buf, const float *nf,
-                                               float *scr, int lane) {
-    if (march_cfg(a)->kpt == 1) march_ray<1>(a, b, buf, nf, scr, lane);
-    else march_ray<2>(a, b, buf, nf, scr, lane);
+                                               float *scr, int lane, bool fine_pass) {
+    if ((fine_pass ? march_cfg(a)->kpt_f : march_cfg(a)->kpt) == 1) march_ray<1>(a, b, buf, nf, scr, lane, fine_pass);
+    else march_ray<2>(a, b, buf, nf, scr, lane, fine_pass);
 }
 
 // PZ: lin_z from the projected latent (gather_proj) instead of the latent gather + GEMM;
@@ -1165,7 +1169,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     const int g = lane >> 4;
     const int cl = lane & 15;
     const Layout &L = a.L;
-    const float *bias = a.packed + L.off_bias;
 
     // per-lane fragment bases
     const int64_t wl_off = (int64_t)(RTW * wave) * 256 + lane * 4;         // f32 fragments
@@ -1268,7 +1271,11 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     float *mreg = PREC == 3 ? hpart + 2048 : petab + 36;
     float *mscr = mreg + MARCH_BUF_FLOATS;
     float *mnf = mscr + 384;
-    const int kpt = MARCH ? march_cfg(a)->kpt : 1;   // tiles per scheduling unit (a ray when marching)
+    const int kpt = MARCH ? march_cfg(a)->kpt : 1;   // tiles per ray and pass when marching
+    // tiles per scheduling unit (a ray when marching): its kpt tiles, and with the single-launch
+    // march (m.single) its kpt_f fine tiles after them
+    const bool single = MARCH && march_cfg(a)->single;
+    const int upt = single ? kpt + march_cfg(a)->kpt_f : kpt;
     // PNR_LOCKSTEP = E > 0 (diagnostic A/B): static per-XCD rounds instead --
     // workgroup j of XCD x takes unit lo_x + r n_x + j in round r -- and every E rounds the
     // XCD's workgroups meet at a spin barrier, so that they run the same layers at the same time
@@ -1276,13 +1283,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // pacing only (no data crosses it): the spin is bounded (50 us) and a timed-out wait proceeds.
     int lk_round = 0;   // tid 0: rounds taken
     auto grab = [&]() -> int {
-        const int64_t T = a.n_tiles >> (kpt - 1);   // kpt is 1 or 2
+        const int64_t T = a.n_tiles / upt;
         if constexpr (PNR_LOCKSTEP > 0) {
             const int x = blockIdx.x & 7, nx = ((int)gridDim.x - x + 7) >> 3, j = blockIdx.x >> 3;
             const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
             const int64_t i = lo + (int64_t)lk_round * nx + j;
             s_next[1] = lk_round++;
-            return i < hi ? (int)(i << (kpt - 1)) : (int)a.n_tiles;
+            return i < hi ? (int)(i * upt) : (int)a.n_tiles;
         }
         const int x0 = blockIdx.x & 7;
         for (int k = 0; k < 8; ++k) {
@@ -1290,7 +1297,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
             if (lo >= hi) continue;
             const int64_t i = lo + atomicAdd(a.tile_ctr + 16 * x, 1);
-            if (i < hi) return (int)(i << (kpt - 1));
+            if (i < hi) return (int)(i * upt);
         }
         return (int)a.n_tiles;
     };
@@ -1299,10 +1306,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     for (int64_t tile = *s_next; tile < a.n_tiles; tile = *s_next) {
         if constexpr (PNR_LOCKSTEP > 0) {
             const int rnd = s_next[1];   // written with s_next, read after the same barrier
-            if ((tile & (kpt - 1)) == 0 && rnd > 0 && rnd % PNR_LOCKSTEP == 0) {
+            if (tile % upt == 0 && rnd > 0 && rnd % PNR_LOCKSTEP == 0) {
                 if (tid == 0) {
                     const int x = blockIdx.x & 7, nx = ((int)gridDim.x - x + 7) >> 3;
-                    const int64_t T = a.n_tiles >> (kpt - 1), lo = x * T / 8, hi = (x + 1) * T / 8;
+                    const int64_t T = a.n_tiles / upt, lo = x * T / 8, hi = (x + 1) * T / 8;
                     const int64_t left = hi - lo - (int64_t)rnd * nx;   // units of this round
                     const int part = left < nx ? (int)left : nx;
                     const int target = (rnd / PNR_LOCKSTEP - 1) * nx + part;
@@ -1316,6 +1323,18 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 lds_barrier();
             }
         }
+        // this tile within its unit: pass_f = a fine tile of the single-launch march; sub = the
+        // tile within its pass (the ray's kpt_t tiles of K_t = 64 kpt_t samples)
+        const int64_t unit = tile / upt;
+        const int s_in = (int)(tile - unit * upt);
+        const bool pass_f = single && s_in >= kpt;
+        const int sub = pass_f ? s_in - kpt : s_in;
+        const int kpt_t = pass_f ? march_cfg(a)->kpt_f : kpt;
+        // the pass's pack and projected latent (read at use: no per-tile SGPR state)
+        auto PK = [&]() -> const float * { return pass_f ? march_cfg(a)->packed_f : a.packed; };
+        auto PJ_ = [&]() -> const float * { return pass_f ? march_cfg(a)->proj_f : a.proj; };
+        const float *bias = PK() + L.off_bias;
+        gc.hdr = PK();
         // per-workgroup scratch (L2-resident): [0] x parked during fc_0, [1] multi-view sum
         // (addresses formed at use: nothing per tile stays live across the GEMMs)
         auto xp_ptr = [&]() { return a.xsum + (int64_t)blockIdx.x * (2 * COLS * H) + wave * (RTW * CT * 256) + opaque_lane(lane) * 4; };
@@ -1332,16 +1351,24 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             float px, py, pz, dx, dy, dz, zz = 0.f;
             int64_t obj;
             if (a.render_mode) {
-                const int64_t b = p / a.K;
+                // ray b, sample kk of its pass (MARCH: the unit's ray, K = 64 kpt_t)
+                const int64_t b = MARCH ? unit : p / a.K;
+                const int kk = MARCH ? sub * COLS + col : (int)(p - b * a.K);
+                const int kt = MARCH ? COLS * kpt_t : a.K;
                 const float *ray = a.rays + b * 8;
-                // the coarse draw in the prologue (nerf.py:98-118), or the given depth
-                if (MARCH && march_cfg(a)->sample_coarse) {
+                if (MARCH && pass_f) {
+                    // single launch: the coarse epilogue left the ray's sorted fine depths in
+                    // mreg (its wave joins this barrier after writing them)
+                    lds_barrier();
+                    zz = mreg[kk];
+                } else if (MARCH && march_cfg(a)->sample_coarse) {
+                    // the coarse draw in the prologue (nerf.py:98-118), or the given depth
                     const CfgPtr m = march_cfg(a);
-                    zz = coarse_z(ld_rng(m->u_coarse), b, a.K, (int)(p - b * a.K), ray[6], ray[7], m->lindisp != 0);
+                    zz = coarse_z(ld_rng(m->u_coarse), b, kt, kk, ray[6], ray[7], m->lindisp != 0);
                     float *zo = m->z_out;
-                    if (zo && qt == 0 && v == 0) zo[p] = zz;
+                    if (zo && qt == 0 && v == 0) zo[b * kt + kk] = zz;
                 } else {
-                    zz = a.zs[p];
+                    zz = a.zs[b * kt + kk];
                 }
                 dx = ray[3]; dy = ray[4]; dz = ray[5];
                 // points = o + z * d  (nerf.py:185)
@@ -1374,9 +1401,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             lds_barrier();   // previous users of inbuf are done
             PT(gc, 10);
             if (MARCH && qt == 0 && v == 0) {   // for the epilogue
-                mreg[(int)(tile & (kpt - 1)) * COLS + col] = zz;
-                if (col == 0 && (tile & (kpt - 1)) == 0) {
-                    const float *rr = a.rays + (tile >> (kpt - 1)) * 8;
+                if (!pass_f) mreg[sub * COLS + col] = zz;
+                if (col == 0 && sub == 0) {
+                    const float *rr = a.rays + unit * 8;
                     mnf[0] = rr[6];
                     mnf[1] = rr[7];
                 }
@@ -1464,14 +1491,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 0);
             // ---- lin_in ---------------------------------------------------------------
             add_bias(x, bias, wave, lane, false);
-            layer_gemm<PREC, NKB_IN, KD>(x, a.packed + L.off_lin_in, gc, 0);
+            layer_gemm<PREC, NKB_IN, KD>(x, PK() + L.off_lin_in, gc, 0);
             // ---- blocks before the combine layer: x += lin_z(z); x = block(x) ------
             for (int blk = 0; blk < L.ncomb; ++blk) {
                 const int lz = layer_index(blk, 0, L.ncomb);
                 if constexpr (PZ) {
                     // the stage aliases the image the previous GEMM read; publish_relu's
                     // internal barrier orders the add_stage reads before the image writes
-                    const float *pz = a.proj + blk * a.proj_stride;
+                    const float *pz = PJ_() + blk * a.proj_stride;
 #if PNR_PROJ_RUNS && !defined(PNR_ABLATE_GATHER)
                     stage_proj_runs(pz, gtab, inbuf, wave, lane);
                     PT(gc, 3);
@@ -1543,31 +1570,31 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 lds_barrier();
                 PT(gc, 1);
                 add_bias(x, bias + (1 + lz) * H, wave, lane, true);
-                layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
+                layer_gemm<PREC, NKB, KD>(x, PK() + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 pre_publish_sync();
                 }
                 HRing<KD> R0;   // fc_0's ring, primed before the publish (PREC 3)
                 if constexpr (PREC == 3)
-                    hring_prime(R0, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                    hring_prime(R0, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
                 f4 nb0[RTW];   // fc_0's bias rows, loaded before the publish too
                 load_bias(nb0, bias + (2 + lz) * H, wave, lane);
                 publish_relu(x, tile, blk, v * P);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 lds_barrier();
                 set_bias(h, nb0, false);
-                layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
+                layer_gemm<PREC, NKB, KD>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
                                           PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
                 if constexpr (PREC == 3)
-                    hring_prime(R1, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                    hring_prime(R1, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off));
                 f4 nb1[RTW];
                 load_bias(nb1, bias + (3 + lz) * H, wave, lane);
                 publish_relu(h, tile, L.n_blocks + blk, v * P);
                 lds_barrier();
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
                 set_bias(x, nb1, true);
-                layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
+                layer_gemm<PREC, NKB, KD>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
                                           PREC == 3 ? &R1 : nullptr);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
@@ -1605,30 +1632,30 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             pre_publish_sync();
             HRing<KD> R0;
             if constexpr (PREC == 3)
-                hring_prime(R0, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off));
+                hring_prime(R0, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off));
             f4 nb0[RTW];
             load_bias(nb0, bias + (1 + l0) * H, wave, lane);
             publish_relu(x, tile, blk, 0);
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
             lds_barrier();
             set_bias(h, nb0, false);
-            layer_gemm<PREC, NKB, KD>(h, a.packed + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
+            layer_gemm<PREC, NKB, KD>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
                                       PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
             HRing<KD> R1;
             if constexpr (PREC == 3)
-                hring_prime(R1, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                hring_prime(R1, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
             f4 nb1[RTW];
             load_bias(nb1, bias + (2 + l0) * H, wave, lane);
             publish_relu(h, tile, L.n_blocks + blk, 0);
             lds_barrier();
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
             set_bias(x, nb1, true);
-            layer_gemm<PREC, NKB, KD>(x, a.packed + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
+            layer_gemm<PREC, NKB, KD>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
                                       PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
-        if (tid == 0) *s_next = (tile + 1) & (kpt - 1) ? tile + 1 : grab();   // read after the closing barrier
+        if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier
         pre_publish_sync();
         publish_relu(x, tile, 2 * L.n_blocks, 0);
         lds_barrier();
@@ -1641,7 +1668,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             // split over the 8 waves: wave w sums column tile w % 4 over k-half w / 4 into LDS;
             // after the tile's closing barrier waves 0-3 add the two halves and apply the head
             const int ct = wave % CT, kh = wave / CT;
-            const float *wo = a.packed + L.off_lin_out + opaque_lane(lane) * 4 + kh * (KS32 / 2) * 512;
+            const float *wo = PK() + L.off_lin_out + opaque_lane(lane) * 4 + kh * (KS32 / 2) * 512;
             const _Float16 *q0 = gc.pb0 + ct * 16 * ROWH + kh * 32 * (KS32 / 2);
             const _Float16 *q1 = gc.pb1 + ct * 16 * ROWH + kh * 32 * (KS32 / 2);
             f4 o = {0.f, 0.f, 0.f, 0.f}, o2 = o;
@@ -1664,7 +1691,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             }
             *reinterpret_cast<f4 *>(hpart + (wave * 64 + opaque_lane(lane)) * 4) = o + o2;
         } else if (PREC != 3 && wave < CT) {   // wave-uniform: the first CT waves own one column tile each
-            const float *wo = a.packed + L.off_lin_out + lane * 4;
+            const float *wo = PK() + L.off_lin_out + lane * 4;
             const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
             f4 o0 = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * g);
             f4 o1 = {0.f, 0.f, 0.f, 0.f}, o2 = o1, o3 = o1;
@@ -1686,7 +1713,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
                 r.w = fmaxf(o.w, 0.f);
                 if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
-                if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * ((int)(tile & (kpt - 1)) * COLS + 16 * wave + cl)) = r;
+                if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * (sub * COLS + 16 * wave + cl)) = r;
             }
         }
         PT(gc, 4);
@@ -1696,7 +1723,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             const int ln = opaque_lane(lane), gg = ln >> 4, cc = ln & 15;
             const f4 h0 = *reinterpret_cast<const f4 *>(hpart + (wave * 64 + ln) * 4);
             const f4 h1 = *reinterpret_cast<const f4 *>(hpart + ((wave + CT) * 64 + ln) * 4);
-            const int e = ecol[16 * wave + cc] + (int)a.packed[HDR_ESCALE + 1 + L.n_l512];
+            const int e = ecol[16 * wave + cc] + (int)PK()[HDR_ESCALE + 1 + L.n_l512];
             const f4 b = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * gg);
             const f4 o = (h0 + h1) * __builtin_ldexpf(1.f, -e) + b;
             const int64_t po = tile * COLS + 16 * wave + cc;
@@ -1707,13 +1734,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
                 r.w = fmaxf(o.w, 0.f);
                 if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
-                if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * ((int)(tile & (kpt - 1)) * COLS + 16 * wave + cc)) = r;
+                if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * (sub * COLS + 16 * wave + cc)) = r;
             }
         }
         // ---- fused march: the ray's last tile composites it (and draws its fine samples) --
-        if (MARCH && ((tile + 1) & (kpt - 1)) == 0) {   // kpt is 1 or 2
+        if (MARCH && sub == kpt_t - 1) {   // the ray's last tile of this pass
             lds_barrier();   // the ray's head outputs visible
-            if (wave == WAVES - 1) march_epilogue(a, tile >> (kpt - 1), mreg, mnf, mscr, opaque_lane(lane));
+            if (wave == WAVES - 1) march_epilogue(a, unit, mreg, mnf, mscr, opaque_lane(lane), pass_f);
         }
     }
 #ifdef PNR_PHASE_TIMING
@@ -2202,6 +2229,12 @@ int launch_point_mlp(const pnr_scene &sc, const pnr_mlp_desc &d, const void *pac
     if (march && (!rays || save || (march->kpt != 1 && march->kpt != 2) || K != mlpk::COLS * march->kpt ||
                   n_points % K != 0 || (march->kf > 0 && (K > 64 || march->n_sort > 128 || K + march->kf > march->n_sort))))
         return fail(PNR_ERR_INVALID, "point_mlp: fused march needs K = 64 kpt (kpt 1 or 2) and kc + kf <= 128");
+    if (march && march->single &&
+        (!proj || !march->packed_f || !march->proj_f || march->kf <= 0 || march->kpt != 1 ||
+         march->kpt_f * mlpk::COLS != K + march->kf || (march->kpt_f != 1 && march->kpt_f != 2) ||
+         !march->rgb_f || !march->depth_f || n_points % (K + march->kpt_f * mlpk::COLS) != 0))
+        return fail(PNR_ERR_INVALID, "point_mlp: the single-launch march needs kc = 64, kc + kf = 64 kpt_f, both "
+                    "packs and projections, fine outputs, and n_points = n_rays (kc + kc + kf)");
     mlpk::Args a = {};
     a.packed = static_cast<const float *>(packed);
     a.L = mlpk::make_layout(d);

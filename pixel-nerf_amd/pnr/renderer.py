@@ -94,7 +94,7 @@ class NeRFRenderer(torch.nn.Module):
         # output dicts (fine-pass parity is classified on them, oracle/parity.py)
         self.return_z = False
         # ray-march schedule of this renderer's fused calls (pnr_render_cfg.march_mode, ABI 3):
-        # None = the library default (pnr_render_set_fused, initially 2), else 0, 1 or 2; all
+        # None = the library default (pnr_render_set_fused, initially 2), else 0, 1, 2 or 3; all
         # give bit-identical results; per call, so renderers in different threads may differ
         self.march_mode = None
 

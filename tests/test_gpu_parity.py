@@ -826,7 +826,7 @@ def test_torch_ops_render_rays_matches_fixture(name):
 def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_views, sb):
     """The fused ray march (pnr_render_set_fused: mode 2, the default, sampling + MLP + composite
     in k_point_mlp with the fine draws in their own kernel; mode 1, the fine draws in the coarse
-    epilogue too) is bit-identical to the separate sample / MLP / composite kernels (mode 0) for
+    epilogue too; mode 3, both passes in one launch for the 64 + 64 shapes) is bit-identical to the separate sample / MLP / composite kernels (mode 0) for
     every output, in every arithmetic; the fixture tests above hold the default path to the
     oracle."""
     from pnr import _lib
@@ -862,7 +862,8 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
     r.return_z = True
     rays = rays.to(DEV).reshape(sb, -1, 8)
     outs = []
-    for mode in (0, 1, 2):   # separate kernels, full fusion, fused passes + fine-draw kernel
+    # separate kernels, full fusion, fused passes + fine-draw kernel, both passes in one launch
+    for mode in (0, 1, 2, 3):
         r.march_mode = mode  # pnr_render_cfg.march_mode (per call, ABI 3)
         with torch.no_grad():
             torch.manual_seed(11)
@@ -876,7 +877,7 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
     for p in (("coarse", "fine") if kf > 0 else ("coarse",)):
         assert torch.equal(dflt[p].rgb, outs[0][p].rgb) and torch.equal(dflt[p].z, outs[0][p].z)
     b = outs[0]
-    for mode, a in ((1, outs[1]), (2, outs[2])):
+    for mode, a in ((1, outs[1]), (2, outs[2]), (3, outs[3])):
         for p in (("coarse", "fine") if kf > 0 else ("coarse",)):
             for k in ("rgb", "depth", "weights", "z"):
                 x, y = getattr(a[p], k, None), getattr(b[p], k, None)

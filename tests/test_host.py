@@ -220,7 +220,8 @@ def test_render_set_fused_modes():
     try:
         assert lib.pnr_render_set_fused(0) == 2
         assert lib.pnr_render_set_fused(1) == 0
-        assert lib.pnr_render_set_fused(7) == 1     # invalid -> default
+        assert lib.pnr_render_set_fused(3) == 1
+        assert lib.pnr_render_set_fused(7) == 3     # invalid -> default
         assert lib.pnr_render_set_fused(2) == 2
         with _lib.fused_march(0):
             assert lib.pnr_render_set_fused(0) == 0
@@ -231,7 +232,7 @@ def test_render_set_fused_modes():
 
 def test_render_cfg_march_mode_is_per_call():
     """ABI 3: pnr_render_cfg.march_mode names the march schedule of one call; a value outside
-    -1..2 is refused before any device work (host-side validation only: the pointers below
+    -1..3 is refused before any device work (host-side validation only: the pointers below
     are never dereferenced), and the refusal does not touch the process default."""
     lib = _lib.load()
     assert ctypes.sizeof(_lib.RenderCfg) == 28
@@ -244,7 +245,7 @@ def test_render_cfg_march_mode_is_per_call():
     out = _lib.RenderOut(p, p, None, p, p, None, None, None)
     prev = lib.pnr_render_set_fused(2)
     try:
-        for bad in (-2, 3, 7):
+        for bad in (-2, 4, 7):
             cfg = _lib.RenderCfg(64, 64, 0, 0.01, 1, 0, bad)
             rc = lib.pnr_render_forward_proj(ctypes.byref(sc), ctypes.byref(desc), p, p, None, None,
                                              ctypes.byref(rays), ctypes.byref(rng), ctypes.byref(cfg),
