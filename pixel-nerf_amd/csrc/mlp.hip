@@ -646,7 +646,10 @@ __device__ __forceinline__ int swz(int col, int k) {
 #endif
 constexpr int H_DIST = PNR_H_DIST;   // f16 weight prefetch distance (row tiles) of the forward:
                                      // 4 measured 1.7 % faster than 3 (5, 6 slower)
-constexpr int H_DIST_3 = 3;          // k_mlp_bwd and the gather-path forward (training):
+#ifndef PNR_H_DIST_3
+#define PNR_H_DIST_3 3
+#endif
+constexpr int H_DIST_3 = PNR_H_DIST_3;          // k_mlp_bwd and the gather-path forward (training):
                                      // 4 spills there
 // The weight register ring of gemm_f16: row tile t = RTW * ks + r of the layer's stream lives
 // in slot t % slots.  hring_prime issues the first DIST row tiles; gemm_f16_primed runs the
