@@ -647,10 +647,11 @@ __device__ __forceinline__ int swz(int col, int k) {
 constexpr int H_DIST = PNR_H_DIST;   // f16 weight prefetch distance (row tiles) of the forward:
                                      // 4 measured 1.7 % faster than 3 (5, 6 slower)
 #ifndef PNR_H_DIST_3
-#define PNR_H_DIST_3 3
+#define PNR_H_DIST_3 4
 #endif
 constexpr int H_DIST_3 = PNR_H_DIST_3;          // k_mlp_bwd and the gather-path forward (training):
-                                     // 4 spills there
+                                     // 4 spills 52-68 B/lane there, yet the training step is 1.2 %
+                                     // faster than with 3 (17.29 -> 17.10 ms, same box, round 3)
 // The weight register ring of gemm_f16: row tile t = RTW * ks + r of the layer's stream lives
 // in slot t % slots.  hring_prime issues the first DIST row tiles; gemm_f16_primed runs the
 // layer on a primed ring.  Priming the next layer's ring before the publish that precedes it
