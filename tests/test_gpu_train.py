@@ -329,10 +329,10 @@ def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K, ns, comb):
 
 @pytest.mark.parametrize("P", [1, 33, 4133, 70000])
 def test_weight_grad_matches_fp64(P):
-    """pnr_weight_grad (split-bf16 x6 on MFMA, point-chunk partials + fixed-order reduce)
-    against an fp64 GEMM: 3 layers, ragged point counts, magnitudes spread over 2^-30 .. 2^10
-    per row (bf16's exponent range, no scaling).  Tolerance 4e-6 of each result's max-abs
-    (fp32 accumulation over up to 70k points)."""
+    """pnr_weight_grad (f16x3 on MFMA with running per-(chunk, channel) power-of-two scales,
+    point-chunk partials + fixed-order reduce) against an fp64 GEMM: 3 layers, ragged point
+    counts, magnitudes spread over 2^-30 .. 2^10 per row.  Tolerance 4e-6 of each result's
+    max-abs (fp32 accumulation over up to 70k points)."""
     from pnr import train
 
     gen = torch.Generator(device="cpu").manual_seed(P)
@@ -350,3 +350,67 @@ def test_weight_grad_matches_fp64(P):
         assert err < 4e-6, (j, err)
     # deterministic: same bits on a second call
     assert torch.equal(train.weight_grad(dys, xs, P), g)
+
+
+@pytest.mark.parametrize("case", ["growing", "late_channels", "huge_tiny", "zeros", "rays"])
+def test_weight_grad_scale_moves(case):
+    """The f16x3 weight gradient's running channel scales (csrc/wgrad.hip k_wgrad_h): data whose
+    channel maxima grow along the points (every chunk moves its scales many times: rows ramp from
+    2^-20 to 2^20), channels that stay zero for the first half of the points and then turn on,
+    channel blocks 2^80 / 2^-60 apart (products from 2^117 down to 2^-113), and all-zero inputs.  Against an fp64 GEMM,
+    4e-6 of each result's max-abs, and deterministic."""
+    from pnr import train
+
+    P = 9000
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    d = torch.randn(P, 512, generator=gen)
+    x = torch.relu(torch.randn(P, 512, generator=gen))
+    if case == "growing":
+        ramp = torch.exp2(torch.linspace(-20, 20, P)).unsqueeze(1)
+        d = d * ramp
+        x = x * ramp.flip(0).sqrt()
+    elif case == "late_channels":
+        d[: P // 2, ::3] = 0.0
+        x[: P // 2, 1::2] = 0.0
+        x[P // 2:, 1::2] *= 1e4
+    elif case == "rays":
+        # a training step's shape: per-point gradient magnitudes spread over 2^-30 .. 1 (the
+        # transmittance along each 64-sample ray), sparse relu activations, channels that turn on
+        k = torch.arange(P)
+        u = torch.rand(P // 64 + 1, generator=gen)
+        d = d * torch.exp2(-30.0 * u[k // 64] * (k % 64).float() / 63.0).unsqueeze(1)
+        x = torch.relu(torch.randn(P, 512, generator=gen) - 1.5)
+        x[: P // 3, 5::7] = 0.0
+    elif case == "huge_tiny":
+        d[:, :64] *= 2.0 ** 80
+        d[:, 64:128] *= 2.0 ** -60
+        x[:, :32] *= 2.0 ** -60
+        x[:, 32:64] *= 2.0 ** 20
+    else:
+        d.zero_()
+        x.zero_()
+    dd, xd = d.to(DEV), x.to(DEV)
+    g = train.weight_grad([dd], [xd], P)[0]
+    ref = d.double().t() @ x.double()
+    if case == "zeros":
+        assert torch.equal(g.cpu(), torch.zeros(512, 512))
+        return
+    assert torch.isfinite(g).all()
+    if case == "huge_tiny":
+        # per block: the blocks' magnitudes differ by up to 2^230
+        for rs in (slice(0, 64), slice(64, 128), slice(128, 512)):
+            for cs in (slice(0, 32), slice(32, 64), slice(64, 512)):
+                r = ref[rs, cs]
+                err = ((g.double().cpu()[rs, cs] - r).abs().max() / r.abs().max()).item()
+                assert err < 4e-6, (rs, cs, err)
+    else:
+        err = ((g.double().cpu() - ref).abs().max() / ref.abs().max()).item()
+        print("weight_grad %s: relative error %.2e" % (case, err))
+        assert err < 4e-6, err
+    if case == "rays":
+        # elementwise, against the fp32 GEMM error scale sum_p |dY_pi| |X_pj|
+        scale = d.double().abs().t() @ x.double().abs()
+        ew = ((g.double().cpu() - ref).abs() / scale.clamp_min(1e-300)).max().item()
+        print("weight_grad rays: max |err| / sum |terms| %.2e" % ew)
+        assert ew < 2.0 ** -17, ew
+    assert torch.equal(train.weight_grad([dd], [xd], P)[0], g)
