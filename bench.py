@@ -407,7 +407,8 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
         dist.barrier()
     elapsed = pdist.max_over_ranks(t1 - t0, dev)
     rays_total = sb * per * steps * world
-    arith = (precision + " forward + f16x3 fused input-gradient chain%s + split-bf16 (x6) weight gradients"
+    arith = (precision + " forward + f16x3 fused input-gradient chain%s + f16x3 weight gradients (running "
+             "per-channel power-of-two scales, csrc/wgrad.hip k_wgrad_h)"
              % (" (NS = %d views)" % ns if ns > 1 else "")
              if precision == "f16x3" else precision + " forward, fp32 GEMM backward")
     return {
