@@ -402,8 +402,9 @@ size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points);
  *   d_weight[j] (512 x 512, [out][in]) = dy[j]^T x[j],
  * dy[j] (n_points x 512) the layer's output gradient (pnr_mlp_backward's slots), x[j]
  * (n_points x 512) its input (the activation save).  dy, x, d_weight are host arrays of
- * n_layers device pointers (16-byte aligned).  Split-bf16 products with fp32 accumulation
- * (fp32-level error); deterministic (fixed reduction order). */
+ * n_layers device pointers (16-byte aligned).  fp16 split products (two parts per operand,
+ * power-of-two scales per point chunk and channel that follow the data) with fp32
+ * accumulation: fp32-level error; deterministic (fixed reduction order). */
 int pnr_weight_grad(const float *const *dy, const float *const *x, float *const *d_weight, int32_t n_layers,
                     int64_t n_points, void *workspace, size_t workspace_bytes, pnr_stream_t stream);
 

@@ -122,7 +122,8 @@ def mlp_backward(mlp, save, d_o, P, ns=1, use_wgrad=False):
 
 def weight_grad(dys, xs, P):
     """``pnr_weight_grad``: G[j] = dys[j]^T xs[j] (512 x 512) for (P, 512) fp32 matrices, in
-    one launch (split-bf16 products, fp32-level error, deterministic)."""
+    one launch (fp16 split products with running per-channel scales, fp32-level error,
+    deterministic; csrc/wgrad.hip k_wgrad_h)."""
     import ctypes
 
     n = len(dys)
@@ -170,7 +171,7 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1):
     source views) runs in one ``pnr_mlp_backward_views`` launch on the forward's split-fp16
     GEMM, which also sums every layer's output gradient over its rows (the bias gradients,
     without re-reading dy); the 512-wide weight gradients are ``pnr_weight_grad`` launches
-    (split-bf16, fp32-level), one per row count (ns P view rows before combine_layer, P
+    (fp16 split products, fp32-level), one per row count (ns P view rows before combine_layer, P
     after), over its per-layer output gradients and the activation save."""
     desc, packed, packed_t = mlp.packed_t(code, precision)
     nb = mlp.n_blocks
