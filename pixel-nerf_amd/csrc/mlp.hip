@@ -672,33 +672,43 @@ __device__ __forceinline__ void hring_load(HRing<DIST> &R, const float *__restri
     R.ra[slot][1] = *reinterpret_cast<const h8 *>(src + 256);
 }
 
-template <int DIST>
-__device__ __forceinline__ void hring_prime(HRing<DIST> &R, const float *__restrict__ wp) {
+// rot: the layer's k-steps run in the rotated order (ks + rot) mod NKS (gemm_f16_primed's EARLY)
+template <int DIST, int NKS = KS32>
+__device__ __forceinline__ void hring_prime(HRing<DIST> &R, const float *__restrict__ wp, int rot = 0) {
 #pragma unroll
-    for (int t = 0; t < DIST; ++t) hring_load(R, wp, t, t / RTW, t % RTW);
+    for (int t = 0; t < DIST; ++t) hring_load(R, wp, t, (t / RTW + rot) & (NKS - 1), t % RTW);
 }
 
-template <int NKS, int DIST = H_DIST>
+// EARLY (after a relu publish, WAVES == 8): the k-steps run in the order (ks + rot) mod NKS with
+// rot = 2 wave, so a wave's first U = 2 k-steps read only the image rows it published itself
+// (rows [64 wave, 64 wave + 64), ordered by its own LDS writes); the workgroup barrier that makes
+// the other waves' rows visible comes after them, and the MFMAs of a wave that finished its
+// publish early run while its SIMD-mate is still splitting (plain s_barrier, no flags).
+template <int NKS, int DIST = H_DIST, bool EARLY = false>
 __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const float *__restrict__ wp,
-                                                const _Float16 *pb0, const _Float16 *pb1) {
+                                                const _Float16 *pb0, const _Float16 *pb1, int rot = 0) {
     constexpr int H_RING = HRing<DIST>::slots;   // register ring slots
     static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
     static_assert(NKS % U == 0, "k-steps");
+    static_assert((NKS & (NKS - 1)) == 0, "rotation mask");
+    static_assert(!EARLY || (U * 32 * WAVES == H && NKS > U), "EARLY: a wave's rows are one iteration");
     // one k-step; ph = ks % U (static), tail = this is one of the last U k-steps
     auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
         constexpr int ph = decltype(ph_tag)::value;
         constexpr bool tail = decltype(tail_tag)::value;
         h8 b0[CT], b1[CT];
+        const int kr = (ks + rot) & (NKS - 1);
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-            b0[c] = *reinterpret_cast<const h8 *>(pb0 + c * 16 * ROWH + 32 * ks);
-            b1[c] = *reinterpret_cast<const h8 *>(pb1 + c * 16 * ROWH + 32 * ks);
+            b0[c] = *reinterpret_cast<const h8 *>(pb0 + c * 16 * ROWH + 32 * kr);
+            b1[c] = *reinterpret_cast<const h8 *>(pb1 + c * 16 * ROWH + 32 * kr);
         }
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const int tn = ph * RTW + r + DIST;            // prefetch target, relative to the iteration
-            if (!tail || tn < U * RTW) hring_load(R, wp, tn % H_RING, ks - ph + tn / RTW, tn % RTW);
+            if (!tail || tn < U * RTW)
+                hring_load(R, wp, tn % H_RING, (ks - ph + tn / RTW + rot) & (NKS - 1), tn % RTW);
             __builtin_amdgcn_sched_barrier(0);
             const h8 *a = R.ra[(ph * RTW + r) % H_RING];
 #pragma unroll
@@ -716,16 +726,20 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
         if constexpr (U > 1) kstep(ks0 + 1, std::integral_constant<int, 1>{}, tail_tag);
     };
 #pragma unroll 1
-    for (int ks = 0; ks + U < NKS; ks += U) iter(ks, std::false_type{});
+    for (int ks = 0; ks + U < NKS; ks += U) {
+        iter(ks, std::false_type{});
+        // EARLY: iteration 0 read the wave's own rows; every wave's rows are published after this
+        if (EARLY && ks == 0) lds_barrier();
+    }
     iter(NKS - U, std::true_type{});
 }
 
-template <int NKS, int DIST = H_DIST>
+template <int NKS, int DIST = H_DIST, bool EARLY = false>
 __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
-                                         const _Float16 *pb1) {
+                                         const _Float16 *pb1, int rot = 0) {
     HRing<DIST> R;
-    hring_prime(R, wp);
-    gemm_f16_primed<NKS, DIST>(acc, R, wp, pb0, pb1);
+    hring_prime<DIST, NKS>(R, wp, rot);
+    gemm_f16_primed<NKS, DIST, EARLY>(acc, R, wp, pb0, pb1, rot);
 }
 
 // 4 (or 8) fp32 values -> scaled fp16 parts written to P0 / P1 at half offset `off`
@@ -765,11 +779,39 @@ __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wav
 
 // after relu_colmax + barrier: relu(acc) (RELU) or acc, * 2^e_col split into P0 / P1 (this
 // wave's rows), e_col -> ecol[column]
+struct ECol {
+    int e[CT];   // scale exponent of column 16 c + (lane & 15)
+};
+// A relu-publish store: lanes g and g ^ 1 (16 apart) hold rows 4g .. 4g + 3 of one column in
+// both parts; one v_permlane16_swap per dword leaves the column's 8-row P0 chunk (16 B, k order)
+// in the even lane and its P1 chunk in the odd one, stored with ONE ds_write_b128 at the lane's
+// plane (Pl: P0 for even g, P1 for odd g).  Eight consecutive lanes then write eight distinct
+// bank quads (the B-read swizzle), where two ds_write_b64 per lane were 2-way bank conflicted:
+// the same bytes at the same addresses, half the LDS-array cycles.
+#ifndef PNR_PUB_B64
+__device__ __forceinline__ void put_split4_pair(_Float16 *Pl, int off, const f4 &v, float s) {
+    u2 p0, p1;
+    split_f16x4(v, s, p0, p1);
+    const auto w0 = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
+    const auto w1 = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<u4 *>(Pl + off) = u4{w0[0], w1[0], w0[1], w1[1]};
+}
+#endif
 template <bool RELU = true>
-__device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
+__device__ __forceinline__ ECol relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
                                                  const float *cmax, int *ecol, int wave, int lane) {
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
+    ECol eo;
+#ifndef PNR_PUB_B64
+    // store bases of row tiles r = 0 and 1 (r + 2: +32 halves, the swizzle only XORs the low two
+    // chunk bits; column tile c: +16 ROWH, the swizzle depends on column bits 2-3 only), so the
+    // 16 stores take constant ds_write offsets
+    _Float16 *Pl = (g & 1) ? P1 : P0;
+    const int kb = 16 * RTW * wave + 4 * (g & ~1);
+    _Float16 *q0 = Pl + cl * ROWH + swz(cl, kb), *q1 = Pl + cl * ROWH + swz(cl, kb + 16);
+#endif
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int col = 16 * c + cl;
@@ -778,13 +820,19 @@ __device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _
         const int e = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
         const float sc = __builtin_ldexpf(1.f, e);
         if (wave == 0 && g == 0) ecol[col] = e;
+        eo.e[c] = e;
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
             const f4 o = RELU ? relu4(v) : v;
+#ifdef PNR_PUB_B64   // A/B: two ds_write_b64 per lane (2-way bank conflicts)
             put_split4(P0, P1, col * ROWH + swz(col, 16 * (RTW * wave + r) + 4 * g), o, sc);
+#else
+            put_split4_pair((r & 1) ? q1 : q0, c * 16 * ROWH + (r >> 1) * 32, o, sc);
+#endif
         }
     }
+    return eo;
 }
 
 // this wave's rows of a bias vector (loaded ahead of use: the loads cross LDS-only barriers)
@@ -819,6 +867,12 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
 #ifndef PNR_LOCKSTEP
 #define PNR_LOCKSTEP 0
 #endif
+// Early GEMM start after each relu publish (gemm_f16_primed's EARLY): 0 restores the barrier
+// between the publish and the GEMM (A/B)
+#ifndef PNR_EARLY_GEMM
+#define PNR_EARLY_GEMM 0
+#endif
+constexpr bool kEarlyGemm = PNR_EARLY_GEMM && WAVES == 8;
 #ifndef PNR_PARK_X
 #define PNR_PARK_X 0
 #endif
@@ -855,7 +909,7 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
 // cycles per phase, summed over workgroups: 0 features/projection, 1 latent gather,
 // 2 GEMMs, 3 glue (bias, relu stores, barriers), 4 lin_out head, 5 GEMM calls, 6 tiles.
 #ifdef PNR_PHASE_TIMING
-constexpr int PT_SLOTS = 16;
+constexpr int PT_SLOTS = 20;
 __device__ unsigned long long g_phase[PT_SLOTS];
 #define PT(gc, i)                                                     \
     do {                                                              \
@@ -879,6 +933,7 @@ struct GemmCtx {
     const float *hdr;         // pack header (PREC 3 weight scale exponents)
     const _Float16 *pb0, *pb1;  // PREC 3: P0 / P1 at (column cl, k 8g)
     const int *ecol;          // PREC 3: scale exponent of each IN column
+    ECol ecl;                 // PREC 3: this lane's columns' exponents from the wave's last publish
     int wave, lane;
 #ifdef PNR_PHASE_TIMING
     uint64_t pt[PT_SLOTS], pt_last;
@@ -1057,7 +1112,10 @@ __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, 
 
 // hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index).
 // R: a ring primed (hring_prime) on this layer's weights, or nullptr (PREC 3 only).
-template <int PREC, int NK, int DIST = H_DIST>
+// EARLY (PREC 3, right after publish_relu, no barrier in between): the column exponents come
+// from the wave's own publish (g.ecl; ecol in LDS is not yet visible) and the GEMM starts on the
+// wave's own rows (gemm_f16_primed), so the barrier after the publish is inside the GEMM.
+template <int PREC, int NK, int DIST = H_DIST, bool EARLY = false>
 __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx,
                                            HRing<DIST> *R = nullptr) {
     PT(g, 3);
@@ -1072,7 +1130,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         float sa[CT], ia[CT];
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-            const int e = g.ecol[16 * c + cl] + ew;
+            const int e = (EARLY ? g.ecl.e[c] : g.ecol[16 * c + cl]) + ew;
             sa[c] = __builtin_ldexpf(1.f, e);
             ia[c] = __builtin_ldexpf(1.f, -e);
         }
@@ -1080,8 +1138,9 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
-        if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
-        else gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1);
+        const int rot = EARLY ? 2 * g.wave : 0;
+        if (R) gemm_f16_primed<NK / 2, DIST, EARLY>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot);
+        else gemm_f16<NK / 2, DIST, EARLY>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -1165,6 +1224,7 @@ __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const f
 template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     constexpr int KD = PZ ? H_DIST : H_DIST_3;   // weight ring distance
+    constexpr bool EG = PREC == 3 && kEarlyGemm;   // early GEMM start after the relu publishes
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
     const int tid = threadIdx.x;
@@ -1199,6 +1259,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
     gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
+    for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
     gc.wave = wave;
     gc.lane = lane;
 #ifdef PNR_PHASE_TIMING
@@ -1244,9 +1305,15 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
 #endif
         if constexpr (PREC == 3) {
+            // (phase-timing slots 17, 13-15, 16: glue split into the ring prime / bias loads
+            // before the publish, colmax VALU, its barrier, the split, the closing barrier)
+            PT(gc, 17);
             relu_colmax(acc, cmax, wave, lane);
+            PT(gc, 13);
             lds_barrier();
-            relu_store_split(acc, P0, P1, cmax, ecol, wave, lane);
+            PT(gc, 14);
+            gc.ecl = relu_store_split(acc, P0, P1, cmax, ecol, wave, lane);
+            PT(gc, 15);
         } else {
             store_relu(acc, inbuf, wave, lane);
         }
@@ -1579,26 +1646,28 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 }
                 HRing<KD> R0;   // fc_0's ring, primed before the publish (PREC 3)
                 if constexpr (PREC == 3)
-                    hring_prime(R0, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                    hring_prime(R0, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
                 f4 nb0[RTW];   // fc_0's bias rows, loaded before the publish too
                 load_bias(nb0, bias + (2 + lz) * H, wave, lane);
                 publish_relu(x, tile, blk, v * P);
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
-                lds_barrier();
+                if constexpr (!EG) lds_barrier();   // EG: inside the GEMM, after the wave's own rows
+                PT(gc, 16);
                 set_bias(h, nb0, false);
-                layer_gemm<PREC, NKB, KD>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
+                layer_gemm<PREC, NKB, KD, EG>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
                                           PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
                 if constexpr (PREC == 3)
-                    hring_prime(R1, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                    hring_prime(R1, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
                 f4 nb1[RTW];
                 load_bias(nb1, bias + (3 + lz) * H, wave, lane);
                 publish_relu(h, tile, L.n_blocks + blk, v * P);
-                lds_barrier();
+                if constexpr (!EG) lds_barrier();
+                PT(gc, 16);
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
                 set_bias(x, nb1, true);
-                layer_gemm<PREC, NKB, KD>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
+                layer_gemm<PREC, NKB, KD, EG>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
                                           PREC == 3 ? &R1 : nullptr);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
@@ -1636,26 +1705,28 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             pre_publish_sync();
             HRing<KD> R0;
             if constexpr (PREC == 3)
-                hring_prime(R0, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off));
+                hring_prime(R0, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
             f4 nb0[RTW];
             load_bias(nb0, bias + (1 + l0) * H, wave, lane);
             publish_relu(x, tile, blk, 0);
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
-            lds_barrier();
+            if constexpr (!EG) lds_barrier();
+            PT(gc, 16);
             set_bias(h, nb0, false);
-            layer_gemm<PREC, NKB, KD>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
+            layer_gemm<PREC, NKB, KD, EG>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
                                       PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
             HRing<KD> R1;
             if constexpr (PREC == 3)
-                hring_prime(R1, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off));
+                hring_prime(R1, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
             f4 nb1[RTW];
             load_bias(nb1, bias + (2 + l0) * H, wave, lane);
             publish_relu(h, tile, L.n_blocks + blk, 0);
-            lds_barrier();
+            if constexpr (!EG) lds_barrier();
+            PT(gc, 16);
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
             set_bias(x, nb1, true);
-            layer_gemm<PREC, NKB, KD>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
+            layer_gemm<PREC, NKB, KD, EG>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
                                       PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
@@ -1663,6 +1734,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         pre_publish_sync();
         publish_relu(x, tile, 2 * L.n_blocks, 0);
         lds_barrier();
+        PT(gc, 16);
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY
         if (0)
@@ -1748,7 +1820,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
     }
 #ifdef PNR_PHASE_TIMING
-    if (threadIdx.x == 0)
+#ifndef PNR_PT_WAVE
+#define PNR_PT_WAVE 0
+#endif
+    if (threadIdx.x == 64 * PNR_PT_WAVE)   // the recorded wave
         for (int i = 0; i < PT_SLOTS; ++i) atomicAdd(&g_phase[i], (unsigned long long)gc.pt[i]);
 #endif
 }
@@ -1887,6 +1962,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
     gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
+    for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
     gc.wave = wave;
     gc.lane = lane;
     // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f; every

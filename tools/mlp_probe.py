@@ -46,8 +46,12 @@ if epi is not None:
 if dbg is not None:
     dbg(ph, 0)
     v = list(ph)
-    v[0] += sum(v[8:13])   # the features phase is stamped in parts (slots 8-12 + 0)
+    v[0] += sum(v[8:13])
+    v[3] += sum(v[13:18])   # the publish parts are glue   # the features phase is stamped in parts (slots 8-12 + 0)
     names = ["features", "gather", "gemm", "glue", "head"]
     tot = sum(v[:5])
-    print("phase cycles/tile (wave 0):", {nm: round(v[i] / max(v[6], 1)) for i, nm in enumerate(names)},
+    extra = {nm: round(v[i] / max(v[6], 1)) for i, nm in [(17, "pre_publish"), (13, "pub_colmax"), (14, "pub_barrier1"),
+                                                              (15, "pub_split"), (16, "pub_barrier2")]}
+    print("publish parts cycles/tile (wave %s, inside glue):" % os.environ.get("PT_WAVE", "0"), extra)
+    print("phase cycles/tile:", {nm: round(v[i] / max(v[6], 1)) for i, nm in enumerate(names)},
           "share:", {nm: round(v[i] / max(tot, 1), 4) for i, nm in enumerate(names)})
