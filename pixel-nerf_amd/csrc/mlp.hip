@@ -812,15 +812,32 @@ __device__ __forceinline__ ECol relu_store_split(const Acc &acc, _Float16 *P0, _
     const int kb = 16 * RTW * wave + 4 * (g & ~1);
     _Float16 *q0 = Pl + cl * ROWH + swz(cl, kb), *q1 = Pl + cl * ROWH + swz(cl, kb + 16);
 #endif
+#ifndef PNR_PUB_INTERLEAVED
+    // every column exponent first: a wave's LDS operations complete in order, so a cmax read
+    // issued after stores waits for them (s_waitcnt lgkmcnt), which serialized the four column
+    // tiles' reads behind the previous tiles' stores
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int col = 16 * c + cl;
         const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
         const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
-        const int e = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
-        const float sc = __builtin_ldexpf(1.f, e);
-        if (wave == 0 && g == 0) ecol[col] = e;
-        eo.e[c] = e;
+        eo.e[c] = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
+    }
+    if (wave == 0 && g == 0) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) ecol[16 * c + cl] = eo.e[c];
+    }
+#endif
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+        const int col = 16 * c + cl;
+#ifdef PNR_PUB_INTERLEAVED   // A/B: each column tile's cmax read after the previous tile's stores
+        const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
+        const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
+        eo.e[c] = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
+        if (wave == 0 && g == 0) ecol[col] = eo.e[c];
+#endif
+        const float sc = __builtin_ldexpf(1.f, eo.e[c]);
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
