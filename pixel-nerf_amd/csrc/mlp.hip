@@ -684,9 +684,22 @@ __device__ __forceinline__ void hring_prime(HRing<DIST> &R, const float *__restr
 // (rows [64 wave, 64 wave + 64), ordered by its own LDS writes); the workgroup barrier that makes
 // the other waves' rows visible comes after them, and the MFMAs of a wave that finished its
 // publish early run while its SIMD-mate is still splitting (plain s_barrier, no flags).
+// Fair pipe sharing between the two waves of a SIMD (waves w and w ^ 4): each GEMM iteration a
+// wave publishes its running iteration count in LDS and takes issue priority 1 while it is behind
+// its SIMD-mate (the count read one iteration earlier), 0 otherwise.  At equal priority the older
+// wave wins every MFMA slot, so without this the younger wave finished each layer alone, with a
+// one-k-step weight prefetch that a solo wave's MFMA rate does not cover.
+struct Fair {
+    int *prog;   // LDS: iteration count per wave (8 ints)
+    int wave, it, mate;
+};
+#ifndef PNR_FAIR
+#define PNR_FAIR 1
+#endif
 template <int NKS, int DIST = H_DIST, bool EARLY = false>
 __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const float *__restrict__ wp,
-                                                const _Float16 *pb0, const _Float16 *pb1, int rot = 0) {
+                                                const _Float16 *pb0, const _Float16 *pb1, int rot = 0,
+                                                Fair *F = nullptr) {
     constexpr int H_RING = HRing<DIST>::slots;   // register ring slots
     static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
@@ -722,6 +735,14 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
         }
     };
     auto iter = [&](int ks0, auto tail_tag) {
+        if (F) {
+            const int it = ++F->it;
+            // the mate's count loaded one iteration ago (its LDS latency passed under the MFMAs)
+            if (it > __builtin_amdgcn_readfirstlane(F->mate)) __builtin_amdgcn_s_setprio(0);
+            else __builtin_amdgcn_s_setprio(1);
+            F->prog[F->wave] = it;
+            F->mate = F->prog[F->wave ^ 4];
+        }
         kstep(ks0, std::integral_constant<int, 0>{}, tail_tag);
         if constexpr (U > 1) kstep(ks0 + 1, std::integral_constant<int, 1>{}, tail_tag);
     };
@@ -732,14 +753,15 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
         if (EARLY && ks == 0) lds_barrier();
     }
     iter(NKS - U, std::true_type{});
+    if (F) __builtin_amdgcn_s_setprio(0);
 }
 
 template <int NKS, int DIST = H_DIST, bool EARLY = false>
 __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
-                                         const _Float16 *pb1, int rot = 0) {
+                                         const _Float16 *pb1, int rot = 0, Fair *F = nullptr) {
     HRing<DIST> R;
     hring_prime<DIST, NKS>(R, wp, rot);
-    gemm_f16_primed<NKS, DIST, EARLY>(acc, R, wp, pb0, pb1, rot);
+    gemm_f16_primed<NKS, DIST, EARLY>(acc, R, wp, pb0, pb1, rot, F);
 }
 
 // 4 (or 8) fp32 values -> scaled fp16 parts written to P0 / P1 at half offset `off`
@@ -795,7 +817,11 @@ __device__ __forceinline__ void put_split4_pair(_Float16 *Pl, int off, const f4 
     const auto w0 = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
     const auto w1 = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
+#ifdef PNR_ABLATE_PUBSTORE   // diagnostic (results invalid): the publish's image stores removed
+    if ((w0[0] ^ w1[0] ^ w0[1] ^ w1[1]) == 0x12345u) *reinterpret_cast<u4 *>(Pl + off) = u4{w0[0], w1[0], w0[1], w1[1]};
+#else
     *reinterpret_cast<u4 *>(Pl + off) = u4{w0[0], w1[0], w0[1], w1[1]};
+#endif
 }
 #endif
 template <bool RELU = true>
@@ -951,6 +977,7 @@ struct GemmCtx {
     const _Float16 *pb0, *pb1;  // PREC 3: P0 / P1 at (column cl, k 8g)
     const int *ecol;          // PREC 3: scale exponent of each IN column
     ECol ecl;                 // PREC 3: this lane's columns' exponents from the wave's last publish
+    Fair fair;                // PREC 3 forward: pipe sharing with the SIMD-mate (fair.prog NULL: off)
     int wave, lane;
 #ifdef PNR_PHASE_TIMING
     uint64_t pt[PT_SLOTS], pt_last;
@@ -1156,8 +1183,9 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
 #pragma unroll
             for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
         const int rot = EARLY ? 2 * g.wave : 0;
-        if (R) gemm_f16_primed<NK / 2, DIST, EARLY>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot);
-        else gemm_f16<NK / 2, DIST, EARLY>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot);
+        Fair *F = g.fair.prog ? &g.fair : nullptr;
+        if (R) gemm_f16_primed<NK / 2, DIST, EARLY>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot, F);
+        else gemm_f16<NK / 2, DIST, EARLY>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot, F);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
@@ -1277,6 +1305,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
     for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
+    gc.fair.prog = nullptr;
+    gc.fair.wave = wave;
+    gc.fair.it = 0;
+    gc.fair.mate = 0;
+    if constexpr (PREC == 3 && PNR_FAIR && WAVES == 8) {
+        gc.fair.prog = reinterpret_cast<int *>(petab + 40);   // petab + 32 / 33: s_next, + 64: hpart
+        if (tid < WAVES) gc.fair.prog[tid] = 0;   // visible after the first barrier
+    }
     gc.wave = wave;
     gc.lane = lane;
 #ifdef PNR_PHASE_TIMING
@@ -1980,6 +2016,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
     for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
+    gc.fair.prog = nullptr;
     gc.wave = wave;
     gc.lane = lane;
     // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f; every

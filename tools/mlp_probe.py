@@ -46,6 +46,9 @@ if epi is not None:
 if dbg is not None:
     dbg(ph, 0)
     v = list(ph)
+    print("features parts cycles/tile:", {nm: round(v[i] / max(v[6], 1)) for i, nm in
+          [(8, "point_loads"), (9, "camera_geometry"), (10, "barrier_in"), (11, "pe_features_split"),
+           (12, "projection"), (0, "barrier_out")]})
     v[0] += sum(v[8:13])
     v[3] += sum(v[13:18])   # the publish parts are glue   # the features phase is stamped in parts (slots 8-12 + 0)
     names = ["features", "gather", "gemm", "glue", "head"]
