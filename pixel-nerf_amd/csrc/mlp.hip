@@ -2017,6 +2017,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     gc.ecol = ecol;
     for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
     gc.fair.prog = nullptr;
+    gc.fair.wave = wave;
+    gc.fair.it = 0;
+    gc.fair.mate = 0;
+    if constexpr (PNR_FAIR && WAVES == 8) {
+        gc.fair.prog = ecol + COLS;   // 8 ints after ecol (the launch's LDS size counts them)
+        if (threadIdx.x < WAVES) gc.fair.prog[threadIdx.x] = 0;
+    }
     gc.wave = wave;
     gc.lane = lane;
     // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f; every
@@ -2330,7 +2337,7 @@ int launch_mlp_bwd(const pnr_mlp_desc &d, const void *packed, const void *packed
         a.bsum = static_cast<float *>(ws);
     }
     // split image P0 + P1, column maxima, exponents = 137,472 B
-    const size_t lds = 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (mlpk::COLS * 8 + mlpk::COLS);
+    const size_t lds = 2 * sizeof(_Float16) * mlpk::PART_HALVES + sizeof(float) * (mlpk::COLS * 8 + mlpk::COLS + 8);
     hipLaunchKernelGGL(mlpk::k_mlp_bwd, dim3((unsigned)grid), dim3(mlpk::NTHR), lds, st, a);
     if (!launch_ok("mlp_bwd")) return PNR_ERR_HIP;
     if (d_bias) {
