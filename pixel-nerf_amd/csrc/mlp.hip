@@ -614,13 +614,39 @@ __device__ __forceinline__ unsigned resid_pk(unsigned h, float x, float y) {
     return d;
 #endif
 }
+// Packed-f32 VALU (v_pk_mul_f32) off the publish and the accumulator scaling: PNR_NO_PK 0
+// restores them (A/B)
+#ifndef PNR_NO_PK
+#define PNR_NO_PK 0
+#endif
+// f16(x s) and f16(x s - h) by v_fma_mix (f32 operands, one RNE rounding of the exact fma): with s
+// a power of two, x s is exact in fp32, so these are the bits of v_cvt_pk_f16_f32(x s) and of
+// resid_pk -- without the v_pk_mul_f32 scaling
+__device__ __forceinline__ unsigned mix_pk(float x, float y, float s) {
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(d) : "v"(x), "v"(s));
+    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(d) : "v"(y), "v"(s));
+    return d;
+}
+__device__ __forceinline__ unsigned mix_resid_pk(unsigned h, float x, float y, float s) {
+    unsigned d;
+    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(d) : "v"(x), "v"(s), "v"(h));
+    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(d) : "v"(y), "v"(s), "v"(h));
+    return d;
+}
 // 4 values * s -> packed fp16 parts (2 dwords each): v_cvt_pk_f16_f32 (RNE), residuals
 __device__ __forceinline__ void split_f16x4(const f4 &v, float s, u2 &p0, u2 &p1) {
+#if PNR_NO_PK
+    const unsigned a0 = mix_pk(v.x, v.y, s), b0 = mix_pk(v.z, v.w, s);
+    p0 = u2{a0, b0};
+    p1 = u2{mix_resid_pk(a0, v.x, v.y, s), mix_resid_pk(b0, v.z, v.w, s)};
+#else
     const f2 a = {v.x * s, v.y * s}, b = {v.z * s, v.w * s};
     const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_convertvector(a, h2));
     const unsigned b0 = __builtin_bit_cast(unsigned, __builtin_convertvector(b, h2));
     p0 = u2{a0, b0};
     p1 = u2{resid_pk(a0, a.x, a.y), resid_pk(b0, b.x, b.y)};
+#endif
 }
 
 // LDS image of the GEMM input in PREC 3: each activation column c scaled by 2^e_c and
@@ -1172,16 +1198,25 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         const int cl = opaque_lane(g.lane) & 15;
         const int ew = (int)g.hdr[HDR_ESCALE + hidx];
         float sa[CT], ia[CT];
+        int e_c[CT];
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             const int e = (EARLY ? g.ecl.e[c] : g.ecol[16 * c + cl]) + ew;
+            e_c[c] = e;
             sa[c] = __builtin_ldexpf(1.f, e);
             ia[c] = __builtin_ldexpf(1.f, -e);
         }
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
-            for (int c = 0; c < CT; ++c) acc[r][c] *= sa[c];
+            for (int c = 0; c < CT; ++c) {
+#if PNR_NO_PK   // one v_ldexp_f32 per value (exact, as the power-of-two multiply)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[r][c][q] = __builtin_ldexpf(acc[r][c][q], e_c[c]);
+#else
+                acc[r][c] *= sa[c];
+#endif
+            }
         const int rot = EARLY ? 2 * g.wave : 0;
         Fair *F = g.fair.prog ? &g.fair : nullptr;
         if (R) gemm_f16_primed<NK / 2, DIST, EARLY>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot, F);
@@ -1189,7 +1224,14 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
-            for (int c = 0; c < CT; ++c) acc[r][c] *= ia[c];
+            for (int c = 0; c < CT; ++c) {
+#if PNR_NO_PK
+#pragma unroll
+                for (int q = 0; q < 4; ++q) acc[r][c][q] = __builtin_ldexpf(acc[r][c][q], -e_c[c]);
+#else
+                acc[r][c] *= ia[c];
+#endif
+            }
     } else {
         gemm_split<NK / 2, PREC>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane);
     }
