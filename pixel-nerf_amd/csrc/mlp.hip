@@ -850,9 +850,14 @@ __device__ __forceinline__ void put_split4_pair(_Float16 *Pl, int off, const f4 
 #endif
 }
 #endif
-template <bool RELU = true>
+struct NoHook {
+    __device__ void operator()(int) const {}
+};
+// pf(c): called before column tile c's stores (k_point_mlp issues the next GEMM's ring prime there)
+template <bool RELU = true, class PF = NoHook>
 __device__ __forceinline__ ECol relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
-                                                 const float *cmax, int *ecol, int wave, int lane) {
+                                                 const float *cmax, int *ecol, int wave, int lane,
+                                                 PF pf = PF{}) {
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
     ECol eo;
@@ -890,6 +895,7 @@ __device__ __forceinline__ ECol relu_store_split(const Acc &acc, _Float16 *P0, _
         if (wave == 0 && g == 0) ecol[col] = eo.e[c];
 #endif
         const float sc = __builtin_ldexpf(1.f, eo.e[c]);
+        pf(c);
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
@@ -942,6 +948,9 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
 #define PNR_EARLY_GEMM 0
 #endif
 constexpr bool kEarlyGemm = PNR_EARLY_GEMM && WAVES == 8;
+#ifndef PNR_SPREAD_PRIME
+#define PNR_SPREAD_PRIME 0
+#endif
 #ifndef PNR_PARK_X
 #define PNR_PARK_X 0
 #endif
@@ -1312,6 +1321,10 @@ template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     constexpr int KD = PZ ? H_DIST : H_DIST_3;   // weight ring distance
     constexpr bool EG = PREC == 3 && kEarlyGemm;   // early GEMM start after the relu publishes
+    // PNR_SPREAD_PRIME (off: 0.5-1 % slower): the next GEMM's ring prime issued inside
+    // the publish's split, one row tile per column tile
+    // (the vector-memory path then works under the split's VALU instead of in a burst before it)
+    constexpr bool SP = PREC == 3 && PNR_SPREAD_PRIME && !EG && KD == CT;
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
     const int tid = threadIdx.x;
@@ -1383,7 +1396,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
             lds_barrier();
     };
-    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
+    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0, auto pf) {
         if (a.save) {
             save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
             save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
@@ -1396,6 +1409,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #pragma unroll
                 for (int c = 0; c < CT; ++c) t += acc[r][c].x + acc[r][c].y + acc[r][c].z + acc[r][c].w;
             cmax[tid & 511] = t;
+            for (int c = 0; c < CT; ++c) pf(c);
             return;
         }
 #endif
@@ -1407,7 +1421,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 13);
             lds_barrier();
             PT(gc, 14);
-            gc.ecl = relu_store_split(acc, P0, P1, cmax, ecol, wave, lane);
+            gc.ecl = relu_store_split(acc, P0, P1, cmax, ecol, wave, lane, pf);
             PT(gc, 15);
         } else {
             store_relu(acc, inbuf, wave, lane);
@@ -1739,12 +1753,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 layer_gemm<PREC, NKB, KD>(x, PK() + L.off_l512 + (int64_t)lz * L.layer_floats, gc, 1 + lz);
                 pre_publish_sync();
                 }
-                HRing<KD> R0;   // fc_0's ring, primed before the publish (PREC 3)
-                if constexpr (PREC == 3)
-                    hring_prime(R0, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+                HRing<KD> R0;   // fc_0's ring, primed before or during the publish (PREC 3)
+                const float *w0p = PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats;
+                if constexpr (PREC == 3 && !SP) hring_prime(R0, w0p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
                 f4 nb0[RTW];   // fc_0's bias rows, loaded before the publish too
                 load_bias(nb0, bias + (2 + lz) * H, wave, lane);
-                publish_relu(x, tile, blk, v * P);
+                publish_relu(x, tile, blk, v * P, [&](int t) {
+                    if constexpr (SP) hring_load(R0, w0p + opaque_lane((int)gc.ws_off), t, 0, t);
+                });
                 if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
                 if constexpr (!EG) lds_barrier();   // EG: inside the GEMM, after the wave's own rows
                 PT(gc, 16);
@@ -1753,11 +1769,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                           PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
-                if constexpr (PREC == 3)
-                    hring_prime(R1, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+                const float *w1p = PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats;
+                if constexpr (PREC == 3 && !SP) hring_prime(R1, w1p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
                 f4 nb1[RTW];
                 load_bias(nb1, bias + (3 + lz) * H, wave, lane);
-                publish_relu(h, tile, L.n_blocks + blk, v * P);
+                publish_relu(h, tile, L.n_blocks + blk, v * P, [&](int t) {
+                    if constexpr (SP) hring_load(R1, w1p + opaque_lane((int)gc.ws_off), t, 0, t);
+                });
                 if constexpr (!EG) lds_barrier();
                 PT(gc, 16);
                 if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
@@ -1799,11 +1817,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             const int l0 = layer_index(blk, 1, L.ncomb);
             pre_publish_sync();
             HRing<KD> R0;
-            if constexpr (PREC == 3)
-                hring_prime(R0, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+            const float *w0p = PK() + L.off_l512 + (int64_t)l0 * L.layer_floats;
+            if constexpr (PREC == 3 && !SP) hring_prime(R0, w0p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
             f4 nb0[RTW];
             load_bias(nb0, bias + (1 + l0) * H, wave, lane);
-            publish_relu(x, tile, blk, 0);
+            publish_relu(x, tile, blk, 0, [&](int t) {
+                if constexpr (SP) hring_load(R0, w0p + opaque_lane((int)gc.ws_off), t, 0, t);
+            });
             if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
             if constexpr (!EG) lds_barrier();
             PT(gc, 16);
@@ -1812,11 +1832,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                       PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
             HRing<KD> R1;
-            if constexpr (PREC == 3)
-                hring_prime(R1, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+            const float *w1p = PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats;
+            if constexpr (PREC == 3 && !SP) hring_prime(R1, w1p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
             f4 nb1[RTW];
             load_bias(nb1, bias + (2 + l0) * H, wave, lane);
-            publish_relu(h, tile, L.n_blocks + blk, 0);
+            publish_relu(h, tile, L.n_blocks + blk, 0, [&](int t) {
+                if constexpr (SP) hring_load(R1, w1p + opaque_lane((int)gc.ws_off), t, 0, t);
+            });
             if constexpr (!EG) lds_barrier();
             PT(gc, 16);
             if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
@@ -1827,7 +1849,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier
         pre_publish_sync();
-        publish_relu(x, tile, 2 * L.n_blocks, 0);
+        publish_relu(x, tile, 2 * L.n_blocks, 0, [](int) {});
         lds_barrier();
         PT(gc, 16);
         PT(gc, 3);
