@@ -4,7 +4,7 @@
 # (tag:args passes extra bench.py arguments to that variant)
 # (libpnr.so carries the soname libpnr.so, so libpnr_torch.so binds to the variant loaded first)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-for round in 1 2; do
+for round in $(seq ${ROUNDS:-2}); do
   for v in ${VARIANTS:-default}; do
     t=${v%%:*}; extra=""; [ "$t" != "$v" ] && extra=${v#*:}
     lib=pixel-nerf_amd/build/$t/libpnr.so
