@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 3
+#define PNR_ABI_VERSION 4   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic) */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -397,16 +397,39 @@ int pnr_mlp_backward_views(const pnr_mlp_desc *desc, const void *packed, const v
 /* Workspace bytes of pnr_weight_grad (n_layers in 1..16); 0 if the sizes are invalid. */
 size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points);
 
+/* Arithmetic of pnr_weight_grad_arith (ABI 4).  fp32 in, fp32 out, fp32 accumulation in both.
+ *   PNR_WGRAD_F16X3  (the default of pnr_weight_grad) every operand scaled by a power of two per
+ *       (point chunk, channel) that follows the data, split into two fp16 parts, 3 products on
+ *       v_mfma_f32_16x16x32_f16.  Error bound PER VALUE, relative to M = the running maximum of
+ *       its channel in its chunk (not to the value itself): 22 significand bits down to 2^-8 M,
+ *       an absolute error below ~2^-30 M beneath that (subnormal fp16 parts), zero below
+ *       ~2^-31 M.  So an output element G_ij is fp32-accurate relative to
+ *       sum_p |dy_pi| M_j + M_i |x_pj| (the scale of its channel pair), and an element built
+ *       ONLY from values far below their channels' maxima (x_j nonzero only where dy_i is
+ *       2^-20 M_i) can carry a large RELATIVE error.  Measured on training-step data at the
+ *       fp32 GEMM error scale (DESIGN.md §3 training path).
+ *   PNR_WGRAD_BF16X6 three exact bf16 parts per operand (fp32's exponent range, no scales), the
+ *       6 largest products on v_mfma_f32_16x16x32_bf16 (dropped terms < 2^-24 |x y|): fp32-level
+ *       error PER ELEMENT relative to sum_p |dy_pi x_pj|, whatever the dynamic range.
+ *       ~1.4x the kernel time of F16X3. */
+#define PNR_WGRAD_F16X3 0
+#define PNR_WGRAD_BF16X6 1
+
 /* Replaces: the weight-gradient GEMMs autograd runs for the 512 x 512 nn.Linear layers of
  * ResnetFC (resnetfc.py:132-184): for each layer j,
  *   d_weight[j] (512 x 512, [out][in]) = dy[j]^T x[j],
  * dy[j] (n_points x 512) the layer's output gradient (pnr_mlp_backward's slots), x[j]
  * (n_points x 512) its input (the activation save).  dy, x, d_weight are host arrays of
- * n_layers device pointers (16-byte aligned).  fp16 split products (two parts per operand,
- * power-of-two scales per point chunk and channel that follow the data) with fp32
- * accumulation: fp32-level error; deterministic (fixed reduction order). */
+ * n_layers device pointers (16-byte aligned).  PNR_WGRAD_F16X3 arithmetic (bound above);
+ * deterministic (fixed reduction order). */
 int pnr_weight_grad(const float *const *dy, const float *const *x, float *const *d_weight, int32_t n_layers,
                     int64_t n_points, void *workspace, size_t workspace_bytes, pnr_stream_t stream);
+
+/* pnr_weight_grad with the arithmetic named per call (PNR_WGRAD_*; another value is
+ * PNR_ERR_INVALID); the same workspace. */
+int pnr_weight_grad_arith(const float *const *dy, const float *const *x, float *const *d_weight,
+                          int32_t n_layers, int64_t n_points, int32_t arith, void *workspace,
+                          size_t workspace_bytes, pnr_stream_t stream);
 
 #ifdef __cplusplus
 }

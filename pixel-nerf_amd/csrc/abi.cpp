@@ -33,7 +33,7 @@ int launch_mlp_bwd(const pnr_mlp_desc &, const void *, const void *, const float
 size_t mlp_bwd_workspace_bytes(const pnr_mlp_desc &, int64_t);
 size_t wgrad_workspace_bytes(int, int64_t);
 int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
-                 hipStream_t);
+                 hipStream_t, int arith);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
                      int, int, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
@@ -289,7 +289,15 @@ size_t pnr_weight_grad_workspace_bytes(int32_t n_layers, int64_t n_points) {
 int pnr_weight_grad(const float *const *dy, const float *const *x, float *const *d_weight, int32_t n_layers,
                     int64_t n_points, void *workspace, size_t workspace_bytes, pnr_stream_t stream) {
     if (!dy || !x || !d_weight) return fail(PNR_ERR_INVALID, "pnr_weight_grad: NULL argument");
-    return launch_wgrad(dy, x, d_weight, n_layers, n_points, workspace, workspace_bytes, (hipStream_t)stream);
+    return launch_wgrad(dy, x, d_weight, n_layers, n_points, workspace, workspace_bytes, (hipStream_t)stream,
+                        PNR_WGRAD_F16X3);
+}
+
+int pnr_weight_grad_arith(const float *const *dy, const float *const *x, float *const *d_weight, int32_t n_layers,
+                          int64_t n_points, int32_t arith, void *workspace, size_t workspace_bytes,
+                          pnr_stream_t stream) {
+    if (!dy || !x || !d_weight) return fail(PNR_ERR_INVALID, "pnr_weight_grad_arith: NULL argument");
+    return launch_wgrad(dy, x, d_weight, n_layers, n_points, workspace, workspace_bytes, (hipStream_t)stream, arith);
 }
 
 // workspace layout of pnr_render_forward

@@ -37,7 +37,14 @@
 // retune.  Every value keeps 22 bits down to 2^-8 of its channel's running maximum, and an
 // absolute error below 2^-30 of that maximum beneath it; the result is acc 2^(E_row + E_col).
 //
-// k_wgrad (PNR_WGRAD_BF16X6 builds, the round-2 kernel): split-bf16 products on
+// Bound of k_wgrad_h, per output element: an element whose terms all come from values far
+// below their channel's running maximum M in the chunk (e.g. X_j nonzero only where dY_i is
+// 2^-20 of M_i) keeps only the absolute error ~2^-30 M of those values, not fp32 relative error:
+// values below 2^-8 M lose low bits (the second fp16 part goes subnormal), values below ~2^-19 M
+// lose the first part's bits too, and below ~2^-30 M they flush to zero.
+// (tests/test_gpu_train.py::test_weight_grad_wide_dynamic_range measures both kernels.)
+//
+// k_wgrad (PNR_WGRAD_BF16X6, ABI 4, per call; the round-2 kernel): split-bf16 products on
 // v_mfma_f32_16x16x32_bf16, three exact bf16 parts per operand and the six largest products
 // (dropped terms < 2^-24 |x y|), no scaling (bf16 has fp32's exponent range); one image set,
 // split and MFMAs separated by two barriers per step.
@@ -542,7 +549,9 @@ size_t wgrad_workspace_bytes(int n_jobs, int64_t n_points) {
 }
 
 int launch_wgrad(const float *const *dy, const float *const *x, float *const *g, int n_jobs, int64_t n_points,
-                 void *ws, size_t ws_bytes, hipStream_t st) {
+                 void *ws, size_t ws_bytes, hipStream_t st, int arith) {
+    if (arith != PNR_WGRAD_F16X3 && arith != PNR_WGRAD_BF16X6)
+        return fail(PNR_ERR_INVALID, "weight grad: arithmetic %d is not PNR_WGRAD_F16X3 / PNR_WGRAD_BF16X6", arith);
     if (n_jobs < 1 || n_jobs > wg::MAX_JOBS) return fail(PNR_ERR_UNSUPPORTED, "weight grad: 1..16 layers");
     if (n_points < 0) return fail(PNR_ERR_INVALID, "weight grad: n_points < 0");
     if (n_points == 0) {
@@ -571,11 +580,11 @@ int launch_wgrad(const float *const *dy, const float *const *x, float *const *g,
     a.chunk_points = ((n_points + a.chunks - 1) / a.chunks + wg::PS - 1) / wg::PS * wg::PS;
     a.partial = static_cast<float *>(ws);
     const int unit_groups = (a.n_units + 7) / 8;   // units padded to a multiple of 8 (one per XCD)
-#ifdef PNR_WGRAD_BF16X6
-    hipLaunchKernelGGL(wg::k_wgrad, dim3((unsigned)(unit_groups * 8 * 4)), dim3(wg::NTHR), wg::LDS_BYTES, st, a);
-#else
-    hipLaunchKernelGGL(wg::k_wgrad_h, dim3((unsigned)(unit_groups * 8 * 4)), dim3(wg::NTHR), wg::LDS_BYTES_H, st, a);
-#endif
+    if (arith == PNR_WGRAD_BF16X6)
+        hipLaunchKernelGGL(wg::k_wgrad, dim3((unsigned)(unit_groups * 8 * 4)), dim3(wg::NTHR), wg::LDS_BYTES, st, a);
+    else
+        hipLaunchKernelGGL(wg::k_wgrad_h, dim3((unsigned)(unit_groups * 8 * 4)), dim3(wg::NTHR), wg::LDS_BYTES_H, st,
+                           a);
     if (!launch_ok("wgrad")) return PNR_ERR_HIP;
     const int64_t nt = (int64_t)n_jobs * (wg::H * wg::H / 4);
     hipLaunchKernelGGL(wg::k_wgrad_reduce, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, o, a.partial,

@@ -54,7 +54,7 @@ class Rng(ctypes.Structure):
 
 # pnr_rng counter-mode stream ids (PNR_RNG_*)
 RNG_U_COARSE, RNG_U_FINE, RNG_U_FINE_JIT, RNG_N_DEPTH = 0, 1, 2, 3
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class RenderCfg(ctypes.Structure):
@@ -124,7 +124,12 @@ SIGNATURES = {
     "pnr_weight_grad_workspace_bytes": (c_size, [c_i32, c_i64]),
     "pnr_weight_grad": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i32, c_i64,
                                 c_vp, c_size, c_vp]),
+    "pnr_weight_grad_arith": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), ctypes.POINTER(c_vp), c_i32,
+                                      c_i64, c_i32, c_vp, c_size, c_vp]),
 }
+
+# pnr_weight_grad_arith arithmetics (PNR_WGRAD_*, ABI 4)
+WGRAD_ARITH = {"f16x3": 0, "bf16x6": 1}
 
 _lib = None
 

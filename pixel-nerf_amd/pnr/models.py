@@ -37,6 +37,32 @@ __all__ = ["PositionalEncoding", "ResnetBlockFC", "ResnetFC", "PixelNeRFNet", "m
 PRECISIONS = {"fp32": 0, "f16x3": 3, "bf16x6": 6, "bf16x9": 9}
 
 
+def _own_params(m):
+    """The parameters registered directly on ``m``.  On an nn.DataParallel replica
+    (torch.nn.parallel.replicate) ``_parameters`` is empty: the broadcast copies are plain
+    attributes, listed in ``_former_parameters``."""
+    if m._parameters or not getattr(m, "_is_replica", False):
+        return list(m._parameters.values())
+    return list(m.__dict__.get("_former_parameters", {}).values())
+
+
+def module_params(mod, skip=None):
+    """``mod.parameters()`` that also works on an nn.DataParallel replica (the tensors the
+    replica's forward reads and autograd differentiates), in registration order; submodules
+    named by ``skip`` (a direct child) are left out."""
+    out, seen = [], set()
+    skip_mod = mod._modules.get(skip) if skip else None
+    excluded = set(id(m) for m in skip_mod.modules()) if skip_mod is not None else set()
+    for m in mod.modules():
+        if id(m) in excluded:
+            continue
+        for p in _own_params(m):
+            if p is not None and id(p) not in seen:
+                seen.add(id(p))
+                out.append(p)
+    return out
+
+
 class PositionalEncoding(nn.Module):
     """NeRF sin/cos encoding (code.py:6-52); cos computed as sin(x + pi/2)."""
 
@@ -165,25 +191,39 @@ class ResnetFC(nn.Module):
         w.pe_freqs, w.pe_phases = p(code._freqs.reshape(-1)), p(code._phases.reshape(-1))
         return w, keep
 
+    def _cached(self, name):
+        """This module's own entry of cache ``name`` (None if absent).  Every cache entry
+        starts with a weak reference to the module that built it: nn.DataParallel's
+        replicas (torch.nn.parallel.replicate -> _replicate_for_data_parallel) start from a
+        copy of the original's __dict__, so without the owner check a replica would find
+        the original's packs, which live on the original's device (nerf.py:354-371)."""
+        c = self.__dict__.get(name)
+        return c if c is not None and c[0]() is self else None
+
     def _pack_key(self, code, precision):
         # the submodule list is cached (nn.Module.parameters() walks and de-duplicates the
         # tree on every call: ~50 us of host time per MLP per render call); each submodule's
-        # _parameters dict is read live, so a reassigned parameter still changes the key
+        # parameter dict is read live, so a reassigned parameter still changes the key.  The
+        # snapshot belongs to the module that took it (a DataParallel replica inherits the
+        # original's snapshot in its __dict__ copy and must take its own).
         snap = self.__dict__.get("_pnr_mods")
-        if snap is None or any(tuple(m._modules.values()) != kids for m, kids in snap):   # submodule swapped
+        if (snap is None or snap[0][0] is not self
+                or any(tuple(m._modules.values()) != kids for m, kids in snap)):   # submodule swapped
             snap = [(m, tuple(m._modules.values())) for m in self.modules()]
             self.__dict__["_pnr_mods"] = snap
-        params = [p for m, _ in snap for p in m._parameters.values() if p is not None]
-        return (precision,) + tuple((p.data_ptr(), p._version) for p in params + [code._freqs, code._phases])
+        params = [p for m, _ in snap for p in _own_params(m) if p is not None]
+        dev = self.lin_out.weight.device
+        return (precision, str(dev)) + tuple((p.data_ptr(), p._version)
+                                             for p in params + [code._freqs, code._phases])
 
     def packed(self, code, precision="fp32"):
         """Packed fragment-order copy of the weights (re-packed when they change).  The
         pack is stream-ordered on the current stream: no host sync (the temporaries stay
         referenced by the cache until the next re-pack)."""
         key = self._pack_key(code, precision)
-        cache = self.__dict__.get("_pnr_pack")
-        if cache is not None and cache[0] == key:
-            return cache[1], cache[2]
+        cache = self._cached("_pnr_pack")
+        if cache is not None and cache[1] == key:
+            return cache[2], cache[3]
         pe_n = int(code._freqs.numel())
         desc = self.desc(pe_n, precision)
         lib = _lib.load()
@@ -194,7 +234,7 @@ class ResnetFC(nn.Module):
         buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
         w, keep = self._weights(code, desc)
         _lib.check(lib.pnr_mlp_pack(w, _lib.ptr(buf), nbytes, _lib.stream_of(dev)), "pnr_mlp_pack")
-        self.__dict__["_pnr_pack"] = (key, desc, buf, keep)
+        self.__dict__["_pnr_pack"] = (weakref.ref(self), key, desc, buf, keep)
         return desc, buf
 
     def packed_t(self, code, precision="f16x3"):
@@ -202,9 +242,9 @@ class ResnetFC(nn.Module):
         packed_t), re-packed with the forward pack."""
         desc, buf = self.packed(code, precision)
         key = self._pack_key(code, precision)
-        cache = self.__dict__.get("_pnr_pack_t")
-        if cache is not None and cache[0] == key:
-            return desc, buf, cache[1]
+        cache = self._cached("_pnr_pack_t")
+        if cache is not None and cache[1] == key:
+            return desc, buf, cache[2]
         lib = _lib.load()
         nbytes = lib.pnr_mlp_packed_t_bytes(desc)
         if nbytes == 0:
@@ -214,7 +254,7 @@ class ResnetFC(nn.Module):
         w, keep = self._weights(code, desc)
         _lib.check(lib.pnr_mlp_pack_t(w, _lib.ptr(buf), _lib.ptr(buf_t), nbytes, _lib.stream_of(dev)),
                    "pnr_mlp_pack_t")
-        self.__dict__["_pnr_pack_t"] = (key, buf_t, keep)
+        self.__dict__["_pnr_pack_t"] = (weakref.ref(self), key, buf_t, keep)
         return desc, buf, buf_t
 
     def latent_proj(self, code, scene, latent):
@@ -226,10 +266,13 @@ class ResnetFC(nn.Module):
         if len(getattr(self, "lin_z", [])) == 0:
             return None
         key = self._pack_key(code, None)
-        cache = self.__dict__.get("_pnr_proj")
-        if (cache is not None and cache[0] == key and cache[1]() is latent
-                and cache[2] == latent._version):
-            return cache[3]
+        cache = self._cached("_pnr_proj")
+        if (cache is not None and cache[1] == key and cache[2]() is latent
+                and cache[3] == latent._version):
+            return cache[4]
+        if latent.device != self.lin_out.weight.device:
+            raise ValueError("pnr: latent on %s but the MLP weights on %s" % (latent.device,
+                                                                              self.lin_out.weight.device))
         desc = self.desc(int(code._freqs.numel()))
         lib = _lib.load()
         nbytes = lib.pnr_latent_project_bytes(scene, desc)
@@ -239,7 +282,7 @@ class ResnetFC(nn.Module):
         w, keep = self._weights(code, desc)
         _lib.check(lib.pnr_latent_project(scene, w, _lib.ptr(buf), nbytes, _lib.stream_of(latent.device)),
                    "pnr_latent_project")
-        self.__dict__["_pnr_proj"] = (key, weakref.ref(latent), latent._version, buf, keep)
+        self.__dict__["_pnr_proj"] = (weakref.ref(self), key, weakref.ref(latent), latent._version, buf, keep)
         return buf
 
     def drop_latent_proj(self):
@@ -310,6 +353,10 @@ class PixelNeRFNet(nn.Module):
         # inference: fold lin_z into the latent once per (scene, weights) and blend four
         # projected rows per point (ResnetFC.latent_proj) instead of the per-point lin_z GEMMs
         self.use_latent_proj = True
+        # arithmetic of the training backward's 512 x 512 weight gradients (pnr_weight_grad_arith):
+        # "f16x3" (fast; fp32-level relative to each channel's scale, include/pnr_abi.h) or
+        # "bf16x6" (fp32-level per element whatever the dynamic range, ~1.4x the kernel time)
+        self.wgrad_arith = "f16x3"
 
     # ---- encode ---------------------------------------------------------------------
     def encode(self, images, poses, focal, z_bounds=None, c=None):
@@ -406,7 +453,7 @@ class PixelNeRFNet(nn.Module):
     def needs_grad(self):
         """Does a forward now have to build the autograd graph (training)?"""
         lat = self.encoder.latent_cl
-        return any(p.requires_grad for n, p in self.named_parameters() if not n.startswith("encoder.")) \
+        return any(p.requires_grad for p in module_params(self, skip="encoder")) \
             or (lat.requires_grad and not self.stop_encoder_grad)
 
     def _require_hip(self):

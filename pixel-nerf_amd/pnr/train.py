@@ -37,8 +37,19 @@ __all__ = ["RenderPoints", "Composite", "mlp_backward", "mlp_backward_fused", "w
 
 
 def mlp_params(mlp):
-    """The ResnetFC parameters in registration order (what autograd tracks)."""
-    return list(mlp.parameters())
+    """The ResnetFC parameters in registration order (what autograd tracks), also on an
+    nn.DataParallel replica (bind_parallel, nerf.py:354-371)."""
+    from .models import module_params
+
+    return module_params(mlp)
+
+
+def _on_device(dev, what, *tensors):
+    """Every tensor handed to a training kernel by pointer must live on the launch device
+    (the torch ops check this in C++, torch_ops.cpp; the ctypes calls check it here)."""
+    for name, t in zip(what.split(), tensors):
+        if t is not None and t.device != dev:
+            raise ValueError("pnr: %s is on %s, the launch device is %s" % (name, t.device, dev))
 
 
 def _save_views(save, P, n_blocks, H=512, ns=1):
@@ -120,10 +131,12 @@ def mlp_backward(mlp, save, d_o, P, ns=1, use_wgrad=False):
     return g, d_feat, dz
 
 
-def weight_grad(dys, xs, P):
-    """``pnr_weight_grad``: G[j] = dys[j]^T xs[j] (512 x 512) for (P, 512) fp32 matrices, in
-    one launch (fp16 split products with running per-channel scales, fp32-level error,
-    deterministic; csrc/wgrad.hip k_wgrad_h)."""
+def weight_grad(dys, xs, P, arith="f16x3"):
+    """``pnr_weight_grad_arith``: G[j] = dys[j]^T xs[j] (512 x 512) for (P, 512) fp32 matrices,
+    in one launch, deterministic.  ``arith`` "f16x3" (default; csrc/wgrad.hip k_wgrad_h): fp16
+    split products with running per-(chunk, channel) scales, fp32-level error relative to the
+    channel scale (include/pnr_abi.h states the bound); "bf16x6" (k_wgrad): split-bf16 products,
+    fp32-level error per element whatever the dynamic range."""
     import ctypes
 
     n = len(dys)
@@ -141,8 +154,8 @@ def weight_grad(dys, xs, P):
         return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
 
     outs = (ctypes.c_void_p * n)(*[out[i].data_ptr() for i in range(n)])
-    _lib.check(lib.pnr_weight_grad(arr(dys), arr(xs), outs, n, P, _lib.ptr(ws), wsb, _lib.stream_of(dev)),
-               "pnr_weight_grad")
+    _lib.check(lib.pnr_weight_grad_arith(arr(dys), arr(xs), outs, n, P, _lib.WGRAD_ARITH[arith], _lib.ptr(ws),
+                                         wsb, _lib.stream_of(dev)), "pnr_weight_grad_arith")
     return out
 
 
@@ -165,7 +178,7 @@ def _tall_mm(a, b):
     return (a.view(s, P // s, a.shape[1]).transpose(1, 2) @ b.view(s, P // s, b.shape[1])).sum(0)
 
 
-def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1):
+def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1, wgrad_arith="f16x3"):
     """``mlp_backward`` for f16x3 models: the input-gradient chain (masks, residual adds,
     every 512-wide W^T GEMM, the summed latent gradient, the view mean's backward for ``ns``
     source views) runs in one ``pnr_mlp_backward_views`` launch on the forward's split-fp16
@@ -180,6 +193,7 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1):
     R = ns * P
     feat, z, slot = _save_views(save, P, nb, ns=ns)
     dev = d_o.device
+    _on_device(dev, "packed packed_t save", packed, packed_t, save)
     d_o = d_o.contiguous()
     dy = torch.empty(2 * nb + 1, R, 512, dtype=torch.float32, device=dev)
     dzl = torch.empty(R, 512, dtype=torch.float32, device=dev) if lin_z else None
@@ -209,7 +223,7 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1):
     for rows, js in jobs.items():
         for i in range(0, len(js), 16):   # pnr_weight_grad: up to 16 layers per launch
             part = js[i:i + 16]
-            gw = weight_grad([d for _, d, _ in part], [x for _, _, x in part], rows)
+            gw = weight_grad([d for _, d, _ in part], [x for _, _, x in part], rows, wgrad_arith)
             for j, (param, _, _) in enumerate(part):
                 g[param] = gw[j]
     for b, blk in enumerate(mlp.blocks):
@@ -239,6 +253,7 @@ class RenderPoints(torch.autograd.Function):
         P = B * K
         lib = _lib.load()
         dev = z.device
+        _on_device(dev, "packed rays latent cams", packed, rays, net.encoder.latent_cl, net.cams)
         ns = net.num_views_per_obj
         save = None
         # no activation save without a backward (no_grad); callers driving forward() by hand
@@ -271,7 +286,8 @@ class RenderPoints(torch.autograd.Function):
                          d_out[:, 3:] * (out[:, 3:] > 0)], dim=1)
         ns = net.num_views_per_obj
         if net.mlp_precision == "f16x3":
-            g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns)
+            g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns,
+                                                   getattr(net, "wgrad_arith", "f16x3"))
         else:
             g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns, use_wgrad=net.mlp_precision == "f16x3")
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
@@ -281,6 +297,8 @@ class RenderPoints(torch.autograd.Function):
             if d_zlat is None:
                 d_zlat = torch.zeros(ns * P, 512, dtype=torch.float32, device=z.device)
             lib = _lib.load()
+            _on_device(z.device, "packed rays d_feat d_zlat d_latent cams latent", ctx.packed, rays, d_feat,
+                       d_zlat, d_lat, net.cams, net.encoder.latent_cl)
             r = _lib.Rays(_lib.ptr(rays), B, B // net.num_objs)
             _lib.check(lib.pnr_points_input_backward(net.hip_scene(), ctx.desc, _lib.ptr(ctx.packed), r,
                                                      _lib.ptr(z), K, _lib.ptr(d_feat.contiguous()),
@@ -309,6 +327,7 @@ class Composite(torch.autograd.Function):
             d_rgb = torch.zeros(B, 3, dtype=torch.float32, device=z.device)
         d_raw = torch.empty(B, K, 4, dtype=torch.float32, device=z.device)
         d_z = torch.empty(B, K, dtype=torch.float32, device=z.device) if ctx.needs_input_grad[0] else None
+        _on_device(z.device, "raw rays d_rgb d_depth d_weights", raw, rays, d_rgb, d_depth, d_w)
         lib = _lib.load()
         _lib.check(lib.pnr_composite_backward(
             _lib.ptr(z), _lib.ptr(raw), _lib.ptr(rays), B, K, int(bool(ctx.white_bkgd)),

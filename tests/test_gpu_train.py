@@ -65,11 +65,12 @@ def oracle_grads(cs):
     return loss.item(), g
 
 
-def hip_grads(cs, precision):
+def hip_grads(cs, precision, wgrad_arith="f16x3"):
     net = PixelNeRFNet(conf())
     net.load_state_dict(cs["sd"], strict=False)
     net = net.to(DEV)
     net.mlp_precision = precision
+    net.wgrad_arith = wgrad_arith
     latent = cs["latent"].to(DEV).requires_grad_(True)
     net.encode_latent(latent, cs["poses"].to(DEV), cs["focal"].to(DEV), (cs["width"], cs["height"]),
                       c=cs["c"].to(DEV), num_objs=cs["poses"].shape[0])
@@ -87,9 +88,9 @@ def hip_grads(cs, precision):
     return loss.item(), g
 
 
-def compare(cs, precision, tol):
+def compare(cs, precision, tol, wgrad_arith="f16x3"):
     ref_loss, ref = oracle_grads(cs)
-    loss, got = hip_grads(cs, precision)
+    loss, got = hip_grads(cs, precision, wgrad_arith)
     assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss), (loss, ref_loss)
     assert set(ref) == set(got), set(ref) ^ set(got)
     worst = []
@@ -103,10 +104,11 @@ def compare(cs, precision, tol):
     print("worst relative gradient error %.3g (%s)" % worst[-1])
 
 
-@pytest.mark.parametrize("precision,tol", [("fp32", 1e-4), ("f16x3", 2e-4)])
-def test_training_step_gradients_match_oracle(precision, tol):
+@pytest.mark.parametrize("precision,tol,wgrad_arith", [("fp32", 1e-4, "f16x3"), ("f16x3", 2e-4, "f16x3"),
+                                                       ("f16x3", 2e-4, "bf16x6")])
+def test_training_step_gradients_match_oracle(precision, tol, wgrad_arith):
     torch.set_num_threads(8)
-    compare(case(), precision, tol)
+    compare(case(), precision, tol, wgrad_arith)
 
 
 def conditioned(sd, margin=3.0, scale=0.1):
@@ -327,8 +329,9 @@ def test_fused_mlp_backward_matches_torch_backward(rays_per_obj, K, ns, comb):
     print("fused MLP backward: worst relative error %.2e" % worst)
 
 
+@pytest.mark.parametrize("arith", ["f16x3", "bf16x6"])
 @pytest.mark.parametrize("P", [1, 33, 4133, 70000])
-def test_weight_grad_matches_fp64(P):
+def test_weight_grad_matches_fp64(P, arith):
     """pnr_weight_grad (f16x3 on MFMA with running per-(chunk, channel) power-of-two scales,
     point-chunk partials + fixed-order reduce) against an fp64 GEMM: 3 layers, ragged point
     counts, magnitudes spread over 2^-30 .. 2^10 per row.  Tolerance 4e-6 of each result's
@@ -342,14 +345,14 @@ def test_weight_grad_matches_fp64(P):
         x = torch.relu(torch.randn(P, 512, generator=gen)) * torch.exp2(-8 * torch.rand(1, 512, generator=gen))
         dys.append(d.to(DEV))
         xs.append(x.to(DEV))
-    g = train.weight_grad(dys, xs, P)
+    g = train.weight_grad(dys, xs, P, arith)
     for j in range(3):
         ref = dys[j].double().t() @ xs[j].double()
         err = ((g[j].double() - ref).abs().max() / ref.abs().max()).item()
-        print("weight_grad P=%d layer %d: relative error %.2e" % (P, j, err))
+        print("weight_grad %s P=%d layer %d: relative error %.2e" % (arith, P, j, err))
         assert err < 4e-6, (j, err)
     # deterministic: same bits on a second call
-    assert torch.equal(train.weight_grad(dys, xs, P), g)
+    assert torch.equal(train.weight_grad(dys, xs, P, arith), g)
 
 
 @pytest.mark.parametrize("case", ["growing", "late_channels", "huge_tiny", "zeros", "rays"])
@@ -414,3 +417,62 @@ def test_weight_grad_scale_moves(case):
         print("weight_grad rays: max |err| / sum |terms| %.2e" % ew)
         assert ew < 2.0 ** -17, ew
     assert torch.equal(train.weight_grad([dd], [xd], P)[0], g)
+
+
+@pytest.mark.parametrize("arith", ["f16x3", "bf16x6"])
+def test_weight_grad_wide_dynamic_range(arith):
+    """an output element built ONLY from values far below their channel's
+    maximum.  dY rows of the "far" points are scaled by 2^-15 .. 2^-25 (per point); X channels
+    j = 0 mod 4 are nonzero only on those far points, so G_ij for those j has no term from a
+    large dY.  bf16x6 (PNR_WGRAD_BF16X6) must hold every element to the fp32 GEMM error scale
+    sum_p |dY_pi||X_pj|; f16x3 (the default) is held to the bound include/pnr_abi.h states: that
+    scale plus ~2^-30 of the channel maxima times the other operand's column sums."""
+    from pnr import train
+
+    P = 9000
+    gen = torch.Generator(device="cpu").manual_seed(21)
+    d = torch.randn(P, 512, generator=gen)
+    x = torch.relu(torch.randn(P, 512, generator=gen)) + 0.1
+    far = torch.rand(P, generator=gen) < 0.5
+    d[far] *= torch.exp2(-15.0 - 10.0 * torch.rand(int(far.sum()), 1, generator=gen))
+    x[~far, 0::4] = 0.0
+    g = train.weight_grad([d.to(DEV)], [x.to(DEV)], P, arith)[0].double().cpu()
+    ref = d.double().t() @ x.double()
+    scale = d.double().abs().t() @ x.double().abs()
+    rel = ((g - ref).abs() / scale.clamp_min(1e-300))
+    worst_far = rel[:, 0::4].max().item()
+    worst_near = torch.cat([rel[:, 1::4], rel[:, 2::4], rel[:, 3::4]], 1).max().item()
+    print("weight_grad %s wide range: max |err| / sum |terms|: far-only columns %.2e, others %.2e" % (
+        arith, worst_far, worst_near))
+    assert worst_near < 2.0 ** -17, worst_near
+    if arith == "bf16x6":
+        assert worst_far < 2.0 ** -17, worst_far
+    else:
+        mi = d.double().abs().max(0).values.unsqueeze(1)          # channel maxima (>= the chunk maxima)
+        mj = x.double().abs().max(0).values.unsqueeze(0)
+        bound = 2.0 ** -17 * scale + 2.0 ** -28 * (mi * x.double().abs().sum(0).unsqueeze(0)
+                                                   + mj * d.double().abs().sum(0).unsqueeze(1))
+        assert bool(((g - ref).abs() <= bound).all()), float(((g - ref).abs() / bound).max())
+    assert torch.equal(train.weight_grad([d.to(DEV)], [x.to(DEV)], P, arith)[0].double().cpu(), g)
+
+
+def test_weight_grad_arith_selects_kernel():
+    """pnr_weight_grad_arith: both arithmetics agree to the fp32 level on ordinary data, and an
+    unknown arithmetic is refused before any device work."""
+    from pnr import train
+
+    P = 2048
+    gen = torch.Generator(device="cpu").manual_seed(3)
+    d = torch.randn(P, 512, generator=gen).to(DEV)
+    x = torch.relu(torch.randn(P, 512, generator=gen)).to(DEV)
+    a = train.weight_grad([d], [x], P, "f16x3")[0]
+    b = train.weight_grad([d], [x], P, "bf16x6")[0]
+    assert ((a - b).abs().max() / b.abs().max()).item() < 4e-6
+    from pnr import _lib
+
+    lib = _lib.load()
+    import ctypes
+
+    arr = (ctypes.c_void_p * 1)(d.data_ptr())
+    rc = lib.pnr_weight_grad_arith(arr, arr, arr, 1, P, 7, None, 0, None)
+    assert rc == -1 and b"arithmetic" in lib.pnr_last_error()
