@@ -68,6 +68,9 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0 # MI355X_MICROARCH.md: Peak BF16 MFMA, dense
 PEAK_BY_PRECISION = {"fp32": (MFMA_F32_PEAK_TFLOPS, 1), "f16x3": (MFMA_BF16_PEAK_TFLOPS / 3, 3),
                      "bf16x6": (MFMA_BF16_PEAK_TFLOPS / 6, 6),
                      "bf16x9": (MFMA_BF16_PEAK_TFLOPS / 9, 9)}
+# the arithmetic type of the path: fp32 in / fp32 out with fp32 accumulation everywhere; the
+# parenthesis names the matrix-core products the fp32 GEMMs are built from (ARITHMETIC)
+DTYPE = {"fp32": "f32", "f16x3": "f32 (f16x3)", "bf16x6": "f32 (bf16x6)", "bf16x9": "f32 (bf16x9)"}
 ARITHMETIC = {
     "fp32": "v_mfma_f32_16x16x4_f32 (fp32 products, fp32 accumulate)",
     "bf16x6": "exact 3-way bf16 split of both fp32 operands, 6 largest products on "
@@ -83,6 +86,18 @@ FLOP_PER_POINT_NS1 = 4761600 + 2101248   # NS*4,761,600 + 2,101,2
 # FLOP the fused kernel executes per point with the projected latent (lin_z folded into the
 # latent per scene): lin_in + 5 blocks x (fc_0 + fc_1) + lin_out
 KERNEL_FLOP_PER_POINT_NS1 = 2 * 42 * 512 + 5 * 2 * 2 * 512 * 512 + 2 * 512 * 4   # 5,289,984
+
+
+def flop_per_point(ns=1, latent_proj=True, n_blocks=5, combine_layer=3, d_in=42):
+    """ResnetFC FLOP per point with ns source views (resnetfc.py:132-184): lin_in, the lin_z
+    GEMMs (not executed with the projected latent: k_latent_proj folds them per latent pixel) and
+    both block layers before combine_layer once per view, the later blocks once per point, lin_out.
+    ns = 1, latent_proj False: FLOP_PER_POINT_NS1; True: KERNEL_FLOP_PER_POINT_NS1."""
+    H = 512
+    nc = min(combine_layer, n_blocks) if ns > 1 else n_blocks
+    nz = min(combine_layer, n_blocks)
+    per_view = 2 * H * d_in + 2 * H * H * (2 * nc + (0 if latent_proj else nz))
+    return ns * per_view + 2 * H * H * 2 * (n_blocks - nc) + 2 * H * 4
 KC, KF = 64, 64
 # cfg3 (headline): ShapeNet-NMR 64x64, 24 target frames, latent 32x32
 NMR_SIZE, NMR_FRAMES, NMR_FOCAL, NMR_NEAR, NMR_FAR, NMR_RADIUS = 64, 24, 70.0, 1.2, 4.0, 2.7
@@ -153,8 +168,9 @@ class RenderProbe:
     def reset(self):
         self.calls = []
 
-    def summary(self, precision, latent_proj):
-        """Per-kernel mean ms, and the fine MLP's roofline over the recorded launches."""
+    def summary(self, precision, latent_proj, ns=1):
+        """Per-kernel mean ms, and the fine MLP's roofline over the recorded launches (ns source
+        views per point: the multi-view FLOP count)."""
         per = {n: [] for n in KERNELS}
         pts = []
         single = False
@@ -165,7 +181,8 @@ class RenderProbe:
             single = FUSED_MARCH and MARCH_MODE == 3 and latent_proj and kc == 64 and kc + kf == 128
             pts.append(n * (kc + kc + kf) if single else n * (kc + kf))
         avg = {k: sum(v) / len(v) for k, v in per.items() if v}
-        kflop = KERNEL_FLOP_PER_POINT_NS1 if latent_proj else FLOP_PER_POINT_NS1
+        kflop = flop_per_point(ns, latent_proj)
+        ref_flop = flop_per_point(ns, False)
         pts_per_launch = sum(pts) / len(pts)
         flop = pts_per_launch * kflop
         ms = avg["mlp_coarse"] if single else avg["mlp_fine"]
@@ -180,7 +197,7 @@ class RenderProbe:
             "achieved": round(achieved, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s (fp32-equivalent: algorithmic FLOP per launch (%d FLOP per point x points "
                     "per launch) / mean launch duration, HIP events on the launch stream)" % kflop,
-            "reference_equivalent_tflops": round(pts_per_launch * FLOP_PER_POINT_NS1 / (ms * 1e-3) / 1e12, 2),
+            "reference_equivalent_tflops": round(pts_per_launch * ref_flop / (ms * 1e-3) / 1e12, 2),
             "frac": round(achieved / peak, 4),
             "mfma_issue": {"tflops": round(achieved * terms, 1),
                            "peak": MFMA_F32_PEAK_TFLOPS if terms == 1 else MFMA_BF16_PEAK_TFLOPS,
@@ -394,6 +411,9 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    from pnr import train as ptrain
+
+    ptrain.KERNEL_EVENTS = None if graph else {}   # HIP events around the MLP kernels (eager only)
     t0 = time.perf_counter()
     if sync_debug:
         torch.cuda.set_sync_debug_mode("warn")
@@ -403,10 +423,34 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
         torch.cuda.set_sync_debug_mode("default")
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    kev, ptrain.KERNEL_EVENTS = ptrain.KERNEL_EVENTS, None
     if world > 1:
         dist.barrier()
     elapsed = pdist.max_over_ranks(t1 - t0, dev)
     rays_total = sb * per * steps * world
+    # roofline of the step: algorithmic FLOP = forward + input gradient + weight gradient of every
+    # ResnetFC layer, 3 x 6,862,848 per point (NS = 1; §8(d)), over the step's points
+    # (SB x B' rays x (64 coarse + 96 fine)); peak = the f16x3 fp32-equivalent 833 TFLOP/s
+    pts = sb * per * (renderer.n_coarse + renderer.n_coarse + renderer.n_fine)
+    step_flop = 3.0 * FLOP_PER_POINT_NS1 * pts * ns if ns == 1 else None
+    ms_step = elapsed / steps * 1e3
+    peak = PEAK_BY_PRECISION[precision][0]
+    roof = None
+    if step_flop is not None:
+        kernels = {}
+        for name, evs in (kev or {}).items():
+            ms = sum(a.elapsed_time(b) for a, b, _ in evs) / steps
+            fl = sum(f for _, _, f in evs) / steps
+            kernels[name] = {"ms_per_step": round(ms, 4), "launches_per_step": len(evs) // steps,
+                             "tflops": round(fl / (ms * 1e-3) / 1e12, 1), "frac": round(fl / (ms * 1e-3) / 1e12 / peak, 4)}
+        roof = {"bound": "mfma", "achieved": round(step_flop / (ms_step * 1e-3) / 1e12, 2), "peak": round(peak, 1),
+                "unit": "TFLOP/s (fp32-equivalent: 3 x %d FLOP per point (forward + input gradient + weight "
+                        "gradient) x %d points per step / ms_per_step)" % (FLOP_PER_POINT_NS1, pts),
+                "frac": round(step_flop / (ms_step * 1e-3) / 1e12 / peak, 4), "flop_per_step": int(step_flop),
+                "kernels": kernels,
+                "kernel_note": "HIP events on the launch stream: forward = k_point_mlp<3, false, false> with the "
+                               "activation save, mlp_backward = k_mlp_bwd (+ k_bias_reduce), weight_grad = "
+                               "k_wgrad_h (+ k_wgrad_reduce); frac of each against the same peak"}
     arith = (precision + " forward + f16x3 fused input-gradient chain%s + f16x3 weight gradients (running "
              "per-channel power-of-two scales, csrc/wgrad.hip k_wgrad_h)"
              % (" (NS = %d views)" % ns if ns > 1 else "")
@@ -423,6 +467,7 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
                                               if bn == "sync" else ""),
                    "launch": "one HIP graph per step" if graph else "eager"},
         "loss": round(float(loss.item()), 6),
+        "roofline": roof,
     }
 
 
@@ -485,11 +530,13 @@ def _time_render(net, renderer, rays, chunk, passes=2):
     return (time.perf_counter() - t0) / passes
 
 
-def extra_configs(dev, precision, latent_proj=True):
+def extra_configs(dev, precision, latent_proj=True, probe=None, oracle_rays=64):
     """Other SURVEY §8(d) workloads on 1 GPU (informational, not `value`): cfg2 with the
     shipped conf (64 + 32 incl. 16 depth samples), cfg2 as eval_approx.py --coarse renders it
     (mlp_fine = None, 64 + 128), cfg4 DTU 400x300 with NS = 3 source views (one 120,000-ray
-    frame, the multi-view mean path) in gen_video's 50,000-ray chunks."""
+    frame, the multi-view mean path) in gen_video's 50,000-ray chunks -- with its fine-launch
+    roofline (HIP events, NS = 3 FLOP per point as the kernel executes it) and an oracle agreement
+    leg on ``oracle_rays`` rays of the frame (the CPU oracle, same injected streams)."""
     res = {}
     sd = synth.pixelnerf_state(1)
 
@@ -519,11 +566,48 @@ def extra_configs(dev, precision, latent_proj=True):
                c=sc["c"][None])
     rays = util.gen_rays(synth.srn_poses([10.0], phi=-12.0, radius=2.0).to(dev), 400, 300, sc["focal"],
                          0.1, 5.0, c=sc["c"]).reshape(-1, 8)
-    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=False).to(dev)
-    s = _time_render(net, r, rays, RAY_BATCH, passes=1)
-    res["cfg4_dtu_ns3_frame"] = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
-                                     gflop_per_ray=round(192 * (3 * 4761600 + 2101248) / 1e9, 4))
+    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=False, eval_batch_size=RAY_BATCH).to(dev)
+    with torch.no_grad():   # warm-up (packs, projections, allocator)
+        r(net, rays[None])
+    torch.cuda.synchronize(dev)
+    if probe is not None:
+        probe.reset()
+        probe.on = True
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        r(net, rays[None])
+        torch.cuda.synchronize(dev)
+        s = time.perf_counter() - t0
+    cfg4 = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
+                gflop_per_ray=round(192 * flop_per_point(3, False) / 1e9, 4),
+                workload="cfg4: DTU 400x300 frame, 3 source views (150x200 latent each), 64 + 64, "
+                         "gen_video's %d-ray chunks" % RAY_BATCH)
+    if probe is not None:
+        probe.on = False
+        avg, roof = probe.summary(precision, latent_proj, ns=3)
+        roof["kernel"] = "k_point_mlp (fine pass, NS = 3: lin_in and blocks 0-2 per view, mean, blocks 3-4)"
+        cfg4["roofline"] = roof
+        cfg4["kernel_ms"] = {k: round(v, 4) for k, v in avg.items()}
+    if oracle_rays:
+        cfg4["oracle_agreement"] = cfg4_oracle_leg(net, rays, sc, sd, dev, oracle_rays)
+    res["cfg4_dtu_ns3_frame"] = cfg4
     return res
+
+
+def cfg4_oracle_leg(net, rays, sc, sd, dev, n):
+    """The HIP render of n rays spread over the cfg4 frame against the CPU oracle's render of the
+    same rays with the same injected streams (NS = 3 multi-view mean path; black background)."""
+    from oracle import ref_cpu
+
+    idx = torch.linspace(0, rays.shape[0] - 1, n).round().long()
+    sub = rays[idx.to(dev)].contiguous()
+    streams = synth.rng_streams(41, n, 64, 64, 0)
+    scene = ref_cpu.Scene(net.encoder.latent.detach().float().cpu().contiguous(), sc["poses"][None],
+                          sc["focal"][None], 400, 300, sc["c"][None])
+    with torch.no_grad():
+        ref = ref_cpu.render(lambda p, c, d: ref_cpu.pixelnerf_forward(sd, scene, p, c, d), sub.cpu()[None],
+                             64, 64, 0, streams, False)
+    return psnr_vs_reference_path(net, sub, ref, streams, dev, sd, scene, white_bkgd=False)
 
 
 L2_PEAK_TBS = 34.5            # MI355X_MICROARCH.md, L2 (per XCD): ~34.5 TB/s aggregate
@@ -643,7 +727,7 @@ def cpu_baselines(sd, nmr, net3, dev, n_rays):
     return base, ref3, idx, st3, scene3
 
 
-def psnr_vs_reference_path(net, rays_dev, ref, streams, dev, sd, scene):
+def psnr_vs_reference_path(net, rays_dev, ref, streams, dev, sd, scene, white_bkgd=True):
     """SURVEY §8(d)'s PSNR delta: the HIP render of the cpu_baseline rays with the SAME
     injected random streams, against the oracle's render of them (oracle/ref_cpu.py, the
     CPU restatement pinned to the reference).  `agreement_db` = PSNR(HIP, oracle);
@@ -654,7 +738,7 @@ def psnr_vs_reference_path(net, rays_dev, ref, streams, dev, sd, scene):
     from oracle import parity
 
     n = rays_dev.shape[0]
-    r = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=True).to(dev)
+    r = NeRFRenderer(n_coarse=KC, n_fine=KF, n_fine_depth=0, white_bkgd=white_bkgd).to(dev)
     r.streams = tuple(t.to(dev) for t in streams)
     r.return_z = True
     with torch.no_grad():
@@ -688,7 +772,7 @@ def psnr_vs_reference_path(net, rays_dev, ref, streams, dev, sd, scene):
     # no ray escapes an output check: a flipped ray's rgb / depth / weights against the oracle
     # fine pass at its own (HIP) fine samples, with each flip's draw-to-boundary distance
     chk = parity.check_flipped_outputs(sd, scene, rays_dev.cpu(), out.fine.z, out.fine.rgb, out.fine.depth,
-                                       out.fine.weights, cls["flip_idx"], n, True,
+                                       out.fine.weights, cls["flip_idx"], n, white_bkgd,
                                        w_coarse_hip=out.coarse.weights, u_fine=streams[1])
     res["fine"]["flipped_rays_vs_oracle_at_own_samples"] = dict(
         ok=chk["ok"], max_abs=chk["max_abs"], bad_rays=chk.get("bad_rays", []),
@@ -800,7 +884,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": DTYPE[args.precision],
         "arithmetic": ARITHMETIC[args.precision],
         "march": ("separate sample / MLP / composite kernels" if args.unfused else
                   "fused (mode 3): ONE k_point_mlp launch per batch -- a ray's coarse tile (coarse draws in "
@@ -834,7 +918,8 @@ def main():
         if not args.no_composite:
             out["composite"] = composite_roofline(dev, ev)
         if not args.no_extra:
-            out["extra_configs"] = extra_configs(dev, args.precision, not args.no_latent_proj)
+            out["extra_configs"] = extra_configs(dev, args.precision, not args.no_latent_proj, probe,
+                                                 0 if args.no_cpu else 64)
         if not args.no_cpu:
             sd = synth.pixelnerf_state(1)
             out["cpu_baseline"], ref, idx, streams, scene3 = cpu_baselines(sd, nmr, net3, dev, args.cpu_rays)

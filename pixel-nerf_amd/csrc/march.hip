@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void k_composite(
             v = rr[k];
         }
         const float delta = sub_rn(zn, zk);
-        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v.w, 0.0f)))) : 0.0f;
+        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v.w, 0.0f)))) : 0.0f;
         const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
         double p = shifted;
 #pragma unroll

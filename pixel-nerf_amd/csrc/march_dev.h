@@ -7,7 +7,7 @@
 
 namespace pnr {
 
-// Diagnostic stamps of the fused epilogue (mlp.hip, -DPNR_EPI_TIMING); no-ops elsewhere.
+// Diagnostic stamps of the fused epilogue (pnr_diag.h, included by mlp.hip); no-ops elsewhere.
 #ifndef EPI_T
 #define EPI_DECL
 #define EPI_T(i) ((void)0)
@@ -59,7 +59,7 @@ __device__ __forceinline__ float composite_wave(int lane, int64_t b, int K, floa
         const bool valid = k < K;
         const float zn = k + 1 >= K ? far : (i + 1 < S ? zk[i + 1] : z_next_lane);
         const float delta = sub_rn(zn, zk[i]);
-        alpha[i] = valid ? sub_rn(1.0f, expf(mul_rn(-delta, fmaxf(v[i].w, 0.0f)))) : 0.0f;
+        alpha[i] = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v[i].w, 0.0f)))) : 0.0f;
         const float shifted = valid ? add_rn(sub_rn(1.0f, alpha[i]), 1e-10f) : 1.0f;
         lp[i + 1] = lp[i] * (double)shifted;
     }
@@ -311,8 +311,10 @@ struct MarchCfg {
     float *weights_f, *rgb_f, *depth_f;      // fine composite outputs (weights_f may be NULL)
 };
 // LDS floats of the fused march region (k_point_mlp): the ray's z (128) | raw (128 x 4), the
-// epilogue scratch w (128) | cdf (128) | sort (128), near / far (4)
+// epilogue scratch w (128) | cdf (128) | sort (128), near / far (4), and with the single-launch
+// march the fine pack's positional-encoding table (32: freqs | phases; the coarse pack's is the
+// kernel's own table)
 constexpr int MARCH_BUF_FLOATS = 640;
-constexpr int MARCH_LDS_FLOATS = MARCH_BUF_FLOATS + 384 + 4;
+constexpr int MARCH_LDS_FLOATS = MARCH_BUF_FLOATS + 384 + 4 + 32;
 
 }  // namespace pnr

@@ -1,34 +1,26 @@
-// Fused per-point pixelNeRF model on gfx950 f32 MFMA.
+// Fused per-point pixelNeRF model and ray march on gfx950 MFMA.
 //
 // Replaces PixelNeRFNet.forward (models.py:146-266) for the shipped conf:
 //   world->camera transform (162-165), positional encoding (code.py:30-42),
 //   view directions (184-196), pinhole projection + bilinear border gather of
 //   the encoder latent (206-221, encoder.py:80-109), ResnetFC (resnetfc.py:132-184)
 //   with the multi-view mean at combine_layer (util.py:461-471), and the
-//   sigmoid/relu head (258-265).
+//   sigmoid/relu head (258-265); with the fused march (Args::march) also the coarse
+//   draws, the composite and the fine draws of NeRFRenderer.forward (nerf.py:251-303).
 //
-// Work decomposition (DESIGN.md §MLP):
-//   * a workgroup = 4 waves (one per SIMD) = a tile of 64 points ("columns").
-//   * every layer is OUT^T (512 x 64) = W (512 x K) * IN^T (K x 64) on
-//     v_mfma_f32_16x16x4_f32.  Wave w owns output rows [128w, 128w+128) for all
-//     64 columns: 8 row tiles x 4 column tiles = 32 accumulators (128 regs).
-//   * IN^T lives in ONE LDS buffer [column][k] (64 x (512+4) fp32 = 132 KB) that
-//     is reused in turn for the PE features, the gathered latent z, relu(x) and
-//     relu(h); B fragments are ds_read_b128 (4 consecutive k of one column).
-//   * W is pre-packed (k_pack) in fragment order [k-block][row tile][lane][4] so
-//     every wave streams its own 8 row tiles with 16-byte coalesced loads straight
-//     into VGPRs, one k-block (16 k) ahead of the MFMAs.  x (the residual stream)
-//     and h stay in accumulator registers for the whole network.
-#ifdef PNR_EPI_TIMING   // diagnostic: wave cycles of the fused epilogue's parts (pnr_debug_epi)
-__device__ unsigned long long g_epi[8];
-#define EPI_DECL uint64_t epi_last_ = __builtin_amdgcn_s_memtime();
-#define EPI_T(i)                                                                  \
-    do {                                                                          \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();                         \
-        if (lane == 0) atomicAdd(&g_epi[i], (unsigned long long)(t_ - epi_last_)); \
-        epi_last_ = t_;                                                           \
-    } while (0)
-#endif
+// Work decomposition:
+//   * a workgroup = 8 waves (two per SIMD) = a tile of 64 points ("columns"); persistent
+//     workgroups, one per CU, take tiles (or a ray's tiles) from per-XCD counters.
+//   * every layer is OUT^T (512 x 64) = W (512 x K) * IN^T (K x 64).  Wave w owns output
+//     rows [64w, 64w + 64) for all 64 columns: 4 row tiles x 4 column tiles = 16
+//     accumulators; x (the residual stream) and h stay in registers for the whole network.
+//   * f16x3 (PREC 3, the default): IN^T lives in LDS already scaled per column and split
+//     into two fp16 planes P0 / P1 by its producer (features, latent stage, relu publish);
+//     W is pre-packed (k_pack_f16) in A-fragment order with a per-layer scale and streamed
+//     from L2 through a register ring H_DIST row tiles ahead of v_mfma_f32_16x16x32_f16.
+//     fp32 (PREC 0) and split-bf16 (PREC 6 / 9) keep an fp32 image and their own GEMMs.
+// Diagnostic build knobs: pnr_diag.h.
+#include "pnr_diag.h"
 #include <cstddef>
 
 #include "march_dev.h"
@@ -40,13 +32,9 @@ constexpr int H = 512;             // d_hidden == d_latent (only width implement
 constexpr int NRT = H / 16;        // 32 row tiles per layer
 constexpr int NKB = H / 16;        // 32 k-blocks (16 k each) for K = 512
 constexpr int NKB_IN = 4;          // lin_in k-blocks (d_in <= 64, zero padded)
-#ifndef PNR_WAVES
-#define PNR_WAVES 8
-#endif
-constexpr int WAVES = PNR_WAVES;   // 8: two waves per SIMD (4: one)
+constexpr int WAVES = 8;           // two waves per SIMD
 constexpr int NTHR = 64 * WAVES;
 constexpr int RTW = NRT / WAVES;   // row tiles per wave (4 at 8 waves)
-static_assert(WAVES == 4 || WAVES == 8, "4 or 8 waves per workgroup");
 constexpr int CT = 4;              // column tiles (16 columns each)
 constexpr int COLS = 16 * CT;      // 64 points per tile
 constexpr int LDS_LD = H + 4;      // floats per column in the LDS activation buffer
@@ -480,10 +468,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 constexpr int STG_FLOATS = CT * 3 * 256;   // one staging buffer: [ct][part][lane][8 bf16]
-#ifndef PNR_A_DIST
-#define PNR_A_DIST 3
-#endif
-constexpr int A_DIST = PNR_A_DIST;                 // weight prefetch distance (row tiles)
+constexpr int A_DIST = 3;                          // weight prefetch distance (row tiles)
 constexpr int A_RING = A_DIST < 4 ? 4 : 8;         // register ring (divides RTW = 8)
 
 // Split-bf16 GEMM: acc[r][c] += sum over the NTERM largest products of the exact
@@ -507,30 +492,18 @@ __device__ __forceinline__ void gemm_split(Acc &acc, const float *__restrict__ w
 #pragma unroll
         for (int q = 0; q < 3; ++q) dst[q] = *reinterpret_cast<const bf8 *>(src + q * 256);
     };
-    // 4 waves: wave w splits all 8 k of column tile w; 8 waves: wave w splits the
-    // k-half w / 4 (4 values per lane) of column tile w % 4
+    // wave w splits the k-half w / 4 (4 values per lane) of column tile w % 4
     auto split_own = [&](int ks, int buf) {
         const float *bp = inbw + 32 * ks;
-        if constexpr (WAVES == 4) {
-            const f4 lo = *reinterpret_cast<const f4 *>(bp);
-            const f4 hi = *reinterpret_cast<const f4 *>(bp + 4);
-            bf8 p0, p1, p2;
-            split3(lo, hi, p0, p1, p2);
-            float *d = stg + buf * STG_FLOATS + wave * 768 + lane * 4;
-            *reinterpret_cast<bf8 *>(d) = p0;
-            *reinterpret_cast<bf8 *>(d + 256) = p1;
-            *reinterpret_cast<bf8 *>(d + 512) = p2;
-        } else {
-            const f4 v = *reinterpret_cast<const f4 *>(bp);
-            unsigned a0, a1, a2, b0, b1, b2;
-            split_pair(v.x, v.y, a0, a1, a2);
-            split_pair(v.z, v.w, b0, b1, b2);
-            typedef unsigned u2 __attribute__((ext_vector_type(2)));
-            float *d = stg + buf * STG_FLOATS + (wave % CT) * 768 + lane * 4 + 2 * (wave / CT);
-            *reinterpret_cast<u2 *>(d) = u2{a0, b0};
-            *reinterpret_cast<u2 *>(d + 256) = u2{a1, b1};
-            *reinterpret_cast<u2 *>(d + 512) = u2{a2, b2};
-        }
+        const f4 v = *reinterpret_cast<const f4 *>(bp);
+        unsigned a0, a1, a2, b0, b1, b2;
+        split_pair(v.x, v.y, a0, a1, a2);
+        split_pair(v.z, v.w, b0, b1, b2);
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        float *d = stg + buf * STG_FLOATS + (wave % CT) * 768 + lane * 4 + 2 * (wave / CT);
+        *reinterpret_cast<u2 *>(d) = u2{a0, b0};
+        *reinterpret_cast<u2 *>(d + 256) = u2{a1, b1};
+        *reinterpret_cast<u2 *>(d + 512) = u2{a2, b2};
     };
     split_own(0, 0);
 #pragma unroll
@@ -603,50 +576,18 @@ __device__ __forceinline__ f4 mfma_h(h8 a, h8 b, f4 c) {
 // (the fp16 operand widened in the instruction, one rounding of the exact difference: the
 // same bits as subtracting in fp32 and converting, in 2 instructions instead of 5)
 __device__ __forceinline__ unsigned resid_pk(unsigned h, float x, float y) {
-#ifdef PNR_NO_FMA_MIX
-    const h2 hh = __builtin_bit_cast(h2, h);
-    const f2 r = f2{x, y} - __builtin_convertvector(hh, f2);
-    return __builtin_bit_cast(unsigned, __builtin_convertvector(r, h2));
-#else
     unsigned d;
     asm("v_fma_mixlo_f16 %0, -%1, 1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(h), "v"(x));
     asm("v_fma_mixhi_f16 %0, -%1, 1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(d) : "v"(h), "v"(y));
     return d;
-#endif
-}
-// Packed-f32 VALU (v_pk_mul_f32) off the publish and the accumulator scaling: PNR_NO_PK 0
-// restores them (A/B)
-#ifndef PNR_NO_PK
-#define PNR_NO_PK 0
-#endif
-// f16(x s) and f16(x s - h) by v_fma_mix (f32 operands, one RNE rounding of the exact fma): with s
-// a power of two, x s is exact in fp32, so these are the bits of v_cvt_pk_f16_f32(x s) and of
-// resid_pk -- without the v_pk_mul_f32 scaling
-__device__ __forceinline__ unsigned mix_pk(float x, float y, float s) {
-    unsigned d;
-    asm("v_fma_mixlo_f16 %0, %1, %2, 0" : "=v"(d) : "v"(x), "v"(s));
-    asm("v_fma_mixhi_f16 %0, %1, %2, 0" : "+v"(d) : "v"(y), "v"(s));
-    return d;
-}
-__device__ __forceinline__ unsigned mix_resid_pk(unsigned h, float x, float y, float s) {
-    unsigned d;
-    asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(d) : "v"(x), "v"(s), "v"(h));
-    asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(d) : "v"(y), "v"(s), "v"(h));
-    return d;
 }
 // 4 values * s -> packed fp16 parts (2 dwords each): v_cvt_pk_f16_f32 (RNE), residuals
 __device__ __forceinline__ void split_f16x4(const f4 &v, float s, u2 &p0, u2 &p1) {
-#if PNR_NO_PK
-    const unsigned a0 = mix_pk(v.x, v.y, s), b0 = mix_pk(v.z, v.w, s);
-    p0 = u2{a0, b0};
-    p1 = u2{mix_resid_pk(a0, v.x, v.y, s), mix_resid_pk(b0, v.z, v.w, s)};
-#else
     const f2 a = {v.x * s, v.y * s}, b = {v.z * s, v.w * s};
     const unsigned a0 = __builtin_bit_cast(unsigned, __builtin_convertvector(a, h2));
     const unsigned b0 = __builtin_bit_cast(unsigned, __builtin_convertvector(b, h2));
     p0 = u2{a0, b0};
     p1 = u2{resid_pk(a0, a.x, a.y), resid_pk(b0, b.x, b.y)};
-#endif
 }
 
 // LDS image of the GEMM input in PREC 3: each activation column c scaled by 2^e_c and
@@ -667,17 +608,9 @@ __device__ __forceinline__ int swz(int col, int k) {
 // stream from L2 A_DIST row tiles ahead; the last k-step is peeled so no load is in
 // flight when the accumulators are handed back.
 //   pb0 / pb1: P0 / P1 at (column cl, k 8g) of column tile 0
-#ifndef PNR_H_DIST
-#define PNR_H_DIST 4
-#endif
-constexpr int H_DIST = PNR_H_DIST;   // f16 weight prefetch distance (row tiles) of the forward:
-                                     // 4 measured 1.7 % faster than 3 (5, 6 slower)
-#ifndef PNR_H_DIST_3
-#define PNR_H_DIST_3 4
-#endif
-constexpr int H_DIST_3 = PNR_H_DIST_3;          // k_mlp_bwd and the gather-path forward (training):
-                                     // 4 spills 52-68 B/lane there, yet the training step is 1.2 %
-                                     // faster than with 3 (17.29 -> 17.10 ms, same box, round 3)
+constexpr int H_DIST = 4;          // f16 weight prefetch distance (row tiles), every kernel: 4 measured
+                                   // 1.7 % faster than 3 on the forward (5, 6 slower), and the training
+                                   // step 1.2 % faster (17.29 -> 17.10 ms) although k_mlp_bwd spills
 // The weight register ring of gemm_f16: row tile t = RTW * ks + r of the layer's stream lives
 // in slot t % slots.  hring_prime issues the first DIST row tiles; gemm_f16_primed runs the
 // layer on a primed ring.  Priming the next layer's ring before the publish that precedes it
@@ -698,18 +631,12 @@ __device__ __forceinline__ void hring_load(HRing<DIST> &R, const float *__restri
     R.ra[slot][1] = *reinterpret_cast<const h8 *>(src + 256);
 }
 
-// rot: the layer's k-steps run in the rotated order (ks + rot) mod NKS (gemm_f16_primed's EARLY)
 template <int DIST, int NKS = KS32>
-__device__ __forceinline__ void hring_prime(HRing<DIST> &R, const float *__restrict__ wp, int rot = 0) {
+__device__ __forceinline__ void hring_prime(HRing<DIST> &R, const float *__restrict__ wp) {
 #pragma unroll
-    for (int t = 0; t < DIST; ++t) hring_load(R, wp, t, (t / RTW + rot) & (NKS - 1), t % RTW);
+    for (int t = 0; t < DIST; ++t) hring_load(R, wp, t, (t / RTW) & (NKS - 1), t % RTW);
 }
 
-// EARLY (after a relu publish, WAVES == 8): the k-steps run in the order (ks + rot) mod NKS with
-// rot = 2 wave, so a wave's first U = 2 k-steps read only the image rows it published itself
-// (rows [64 wave, 64 wave + 64), ordered by its own LDS writes); the workgroup barrier that makes
-// the other waves' rows visible comes after them, and the MFMAs of a wave that finished its
-// publish early run while its SIMD-mate is still splitting (plain s_barrier, no flags).
 // Fair pipe sharing between the two waves of a SIMD (waves w and w ^ 4): each GEMM iteration a
 // wave publishes its running iteration count in LDS and takes issue priority 1 while it is behind
 // its SIMD-mate (the count read one iteration earlier), 0 otherwise.  At equal priority the older
@@ -719,25 +646,20 @@ struct Fair {
     int *prog;   // LDS: iteration count per wave (8 ints)
     int wave, it, mate;
 };
-#ifndef PNR_FAIR
-#define PNR_FAIR 1
-#endif
-template <int NKS, int DIST = H_DIST, bool EARLY = false>
+template <int NKS, int DIST = H_DIST>
 __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const float *__restrict__ wp,
-                                                const _Float16 *pb0, const _Float16 *pb1, int rot = 0,
-                                                Fair *F = nullptr) {
+                                                const _Float16 *pb0, const _Float16 *pb1, Fair *F = nullptr) {
     constexpr int H_RING = HRing<DIST>::slots;   // register ring slots
     static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
     static_assert(NKS % U == 0, "k-steps");
     static_assert((NKS & (NKS - 1)) == 0, "rotation mask");
-    static_assert(!EARLY || (U * 32 * WAVES == H && NKS > U), "EARLY: a wave's rows are one iteration");
     // one k-step; ph = ks % U (static), tail = this is one of the last U k-steps
     auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
         constexpr int ph = decltype(ph_tag)::value;
         constexpr bool tail = decltype(tail_tag)::value;
         h8 b0[CT], b1[CT];
-        const int kr = (ks + rot) & (NKS - 1);
+        const int kr = ks & (NKS - 1);
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             b0[c] = *reinterpret_cast<const h8 *>(pb0 + c * 16 * ROWH + 32 * kr);
@@ -747,7 +669,7 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
         for (int r = 0; r < RTW; ++r) {
             const int tn = ph * RTW + r + DIST;            // prefetch target, relative to the iteration
             if (!tail || tn < U * RTW)
-                hring_load(R, wp, tn % H_RING, (ks - ph + tn / RTW + rot) & (NKS - 1), tn % RTW);
+                hring_load(R, wp, tn % H_RING, (ks - ph + tn / RTW) & (NKS - 1), tn % RTW);
             __builtin_amdgcn_sched_barrier(0);
             const h8 *a = R.ra[(ph * RTW + r) % H_RING];
 #pragma unroll
@@ -773,21 +695,17 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
         if constexpr (U > 1) kstep(ks0 + 1, std::integral_constant<int, 1>{}, tail_tag);
     };
 #pragma unroll 1
-    for (int ks = 0; ks + U < NKS; ks += U) {
-        iter(ks, std::false_type{});
-        // EARLY: iteration 0 read the wave's own rows; every wave's rows are published after this
-        if (EARLY && ks == 0) lds_barrier();
-    }
+    for (int ks = 0; ks + U < NKS; ks += U) iter(ks, std::false_type{});
     iter(NKS - U, std::true_type{});
     if (F) __builtin_amdgcn_s_setprio(0);
 }
 
-template <int NKS, int DIST = H_DIST, bool EARLY = false>
+template <int NKS, int DIST = H_DIST>
 __device__ __forceinline__ void gemm_f16(Acc &acc, const float *__restrict__ wp, const _Float16 *pb0,
-                                         const _Float16 *pb1, int rot = 0, Fair *F = nullptr) {
+                                         const _Float16 *pb1, Fair *F = nullptr) {
     HRing<DIST> R;
-    hring_prime<DIST, NKS>(R, wp, rot);
-    gemm_f16_primed<NKS, DIST, EARLY>(acc, R, wp, pb0, pb1, rot, F);
+    hring_prime<DIST, NKS>(R, wp);
+    gemm_f16_primed<NKS, DIST>(acc, R, wp, pb0, pb1, F);
 }
 
 // 4 (or 8) fp32 values -> scaled fp16 parts written to P0 / P1 at half offset `off`
@@ -812,34 +730,28 @@ __device__ __forceinline__ void relu_colmax(const Acc &acc, float *cmax, int wav
             if constexpr (!RELU) v = f4{fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
             m = max3_nc(max3_nc(m, v.x, v.y), v.z, v.w);
         }
-#ifdef PNR_SHFL_COLMAX
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        m = fmaxf(m, __shfl_xor(m, 32, 64));
-#else
         m = rows_max(m);
-#endif
-        if (g == 0) {
-            cmax[(16 * c + cl) * 8 + wave] = m;
-            if constexpr (WAVES == 4) cmax[(16 * c + cl) * 8 + wave + 4] = m;
-        }
+        if (g == 0) cmax[(16 * c + cl) * 8 + wave] = m;
     }
 }
 
 // after relu_colmax + barrier: relu(acc) (RELU) or acc, * 2^e_col split into P0 / P1 (this
-// wave's rows), e_col -> ecol[column]
-struct ECol {
-    int e[CT];   // scale exponent of column 16 c + (lane & 15)
-};
+// wave's rows), e_col -> ecol[column] (LDS, wave 0) and -> e_col (this lane's columns 16 c + cl:
+// every wave computes the same exponents, so the next GEMM takes them from registers)
 // A relu-publish store: lanes g and g ^ 1 (16 apart) hold rows 4g .. 4g + 3 of one column in
 // both parts; one v_permlane16_swap per dword leaves the column's 8-row P0 chunk (16 B, k order)
 // in the even lane and its P1 chunk in the odd one, stored with ONE ds_write_b128 at the lane's
 // plane (Pl: P0 for even g, P1 for odd g).  Eight consecutive lanes then write eight distinct
 // bank quads (the B-read swizzle), where two ds_write_b64 per lane were 2-way bank conflicted:
 // the same bytes at the same addresses, half the LDS-array cycles.
-#ifndef PNR_PUB_B64
 __device__ __forceinline__ void put_split4_pair(_Float16 *Pl, int off, const f4 &v, float s) {
     u2 p0, p1;
+#ifdef PNR_ABLATE_PUBSPLIT   // diagnostic (results invalid): the value bits stored, no split VALU
+    p0 = u2{__float_as_uint(v.x), __float_as_uint(v.y)};
+    p1 = u2{__float_as_uint(v.z), __float_as_uint(v.w)};
+#else
     split_f16x4(v, s, p0, p1);
+#endif
     const auto w0 = __builtin_amdgcn_permlane16_swap(p0.x, p1.x, false, false);
     const auto w1 = __builtin_amdgcn_permlane16_swap(p0.y, p1.y, false, false);
     typedef unsigned u4 __attribute__((ext_vector_type(4)));
@@ -849,65 +761,51 @@ __device__ __forceinline__ void put_split4_pair(_Float16 *Pl, int off, const f4 
     *reinterpret_cast<u4 *>(Pl + off) = u4{w0[0], w1[0], w0[1], w1[1]};
 #endif
 }
-#endif
-struct NoHook {
-    __device__ void operator()(int) const {}
-};
-// pf(c): called before column tile c's stores (k_point_mlp issues the next GEMM's ring prime there)
-template <bool RELU = true, class PF = NoHook>
-__device__ __forceinline__ ECol relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
+template <bool RELU = true>
+__device__ __forceinline__ void relu_store_split(const Acc &acc, _Float16 *P0, _Float16 *P1,
                                                  const float *cmax, int *ecol, int wave, int lane,
-                                                 PF pf = PF{}) {
+                                                 int (&e_col)[CT]) {
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
-    ECol eo;
-#ifndef PNR_PUB_B64
     // store bases of row tiles r = 0 and 1 (r + 2: +32 halves, the swizzle only XORs the low two
     // chunk bits; column tile c: +16 ROWH, the swizzle depends on column bits 2-3 only), so the
     // 16 stores take constant ds_write offsets
     _Float16 *Pl = (g & 1) ? P1 : P0;
     const int kb = 16 * RTW * wave + 4 * (g & ~1);
     _Float16 *q0 = Pl + cl * ROWH + swz(cl, kb), *q1 = Pl + cl * ROWH + swz(cl, kb + 16);
-#endif
-#ifndef PNR_PUB_INTERLEAVED
     // every column exponent first: a wave's LDS operations complete in order, so a cmax read
     // issued after stores waits for them (s_waitcnt lgkmcnt), which serialized the four column
     // tiles' reads behind the previous tiles' stores
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int col = 16 * c + cl;
+#ifdef PNR_ABLATE_CMAXREAD   // diagnostic (results invalid): no column-maximum reads
+        e_col[c] = 2 + (cl & 1);
+#else
         const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
         const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
-        eo.e[c] = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
+        e_col[c] = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
+#endif
     }
     if (wave == 0 && g == 0) {
 #pragma unroll
-        for (int c = 0; c < CT; ++c) ecol[16 * c + cl] = eo.e[c];
+        for (int c = 0; c < CT; ++c) ecol[16 * c + cl] = e_col[c];
     }
-#endif
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int col = 16 * c + cl;
-#ifdef PNR_PUB_INTERLEAVED   // A/B: each column tile's cmax read after the previous tile's stores
-        const f4 m0 = *reinterpret_cast<const f4 *>(cmax + col * 8);
-        const f4 m1 = *reinterpret_cast<const f4 *>(cmax + col * 8 + 4);
-        eo.e[c] = scale_exp(max3_nc(max3_nc(m0.x, m0.y, m0.z), max3_nc(m0.w, m1.x, m1.y), max_nc(m1.z, m1.w)));
-        if (wave == 0 && g == 0) ecol[col] = eo.e[c];
-#endif
-        const float sc = __builtin_ldexpf(1.f, eo.e[c]);
-        pf(c);
+        const float sc = __builtin_ldexpf(1.f, e_col[c]);
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
-            const f4 o = RELU ? relu4(v) : v;
-#ifdef PNR_PUB_B64   // A/B: two ds_write_b64 per lane (2-way bank conflicts)
-            put_split4(P0, P1, col * ROWH + swz(col, 16 * (RTW * wave + r) + 4 * g), o, sc);
+#ifdef PNR_ABLATE_PUBSPLIT
+            const f4 o = v;
 #else
-            put_split4_pair((r & 1) ? q1 : q0, c * 16 * ROWH + (r >> 1) * 32, o, sc);
+            const f4 o = RELU ? relu4(v) : v;
 #endif
+            put_split4_pair((r & 1) ? q1 : q0, c * 16 * ROWH + (r >> 1) * 32, o, sc);
         }
     }
-    return eo;
 }
 
 // this wave's rows of a bias vector (loaded ahead of use: the loads cross LDS-only barriers)
@@ -939,37 +837,6 @@ __device__ __forceinline__ void add_bias(Acc &acc, const float *__restrict__ bia
     }
 }
 
-#ifndef PNR_LOCKSTEP
-#define PNR_LOCKSTEP 0
-#endif
-// Early GEMM start after each relu publish (gemm_f16_primed's EARLY): 0 restores the barrier
-// between the publish and the GEMM (A/B)
-#ifndef PNR_EARLY_GEMM
-#define PNR_EARLY_GEMM 0
-#endif
-constexpr bool kEarlyGemm = PNR_EARLY_GEMM && WAVES == 8;
-#ifndef PNR_SPREAD_PRIME
-#define PNR_SPREAD_PRIME 0
-#endif
-#ifndef PNR_PARK_X
-#define PNR_PARK_X 0
-#endif
-constexpr bool kParkX = PNR_PARK_X;
-// x parks in scratch while h occupies the accumulator registers (frees 128 regs
-// for the operand pipelines); each (r, c) is one coalesced 1 KB wave store / load
-__device__ __forceinline__ void park(const Acc &acc, float *xp) {
-#pragma unroll
-    for (int r = 0; r < RTW; ++r)
-#pragma unroll
-        for (int c = 0; c < CT; ++c) *reinterpret_cast<f4 *>(xp + (r * CT + c) * 256) = acc[r][c];
-}
-__device__ __forceinline__ void unpark(Acc &acc, const float *xp) {
-#pragma unroll
-    for (int r = 0; r < RTW; ++r)
-#pragma unroll
-        for (int c = 0; c < CT; ++c) acc[r][c] = *reinterpret_cast<const f4 *>(xp + (r * CT + c) * 256);
-}
-
 // IN^T[column][row] = relu(acc) for this wave's rows (4 consecutive rows per lane)
 __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wave, int lane) {
     const int g = lane >> 4, cl = lane & 15;
@@ -978,29 +845,14 @@ __device__ __forceinline__ void store_relu(const Acc &acc, float *inbuf, int wav
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             const f4 v = acc[r][c];
-            f4 o = {fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+            const f4 o = relu4(v);
             *reinterpret_cast<f4 *>(inbuf + (16 * c + cl) * LDS_LD + 16 * (RTW * wave + r) + 4 * g) = o;
         }
 }
 
-// Diagnostic build only (-DPNR_PHASE_TIMING, scripts/build_variant.sh): wave-0 shader
-// cycles per phase, summed over workgroups: 0 features/projection, 1 latent gather,
-// 2 GEMMs, 3 glue (bias, relu stores, barriers), 4 lin_out head, 5 GEMM calls, 6 tiles.
-#ifdef PNR_PHASE_TIMING
+#ifdef PNR_PHASE_TIMING   // pnr_diag.h
 constexpr int PT_SLOTS = 20;
 __device__ unsigned long long g_phase[PT_SLOTS];
-#define PT(gc, i)                                                     \
-    do {                                                              \
-        const uint64_t t_ = __builtin_amdgcn_s_memtime();             \
-        (gc).pt[i] += t_ - (gc).pt_last;                              \
-        (gc).pt_last = t_;                                            \
-    } while (0)
-#define PT_COUNT(gc, i) ((gc).pt[i] += 1)
-#define PT_WAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
-#else
-#define PT_WAIT() ((void)0)
-#define PT(gc, i) ((void)0)
-#define PT_COUNT(gc, i) ((void)0)
 #endif
 
 struct GemmCtx {
@@ -1011,7 +863,7 @@ struct GemmCtx {
     const float *hdr;         // pack header (PREC 3 weight scale exponents)
     const _Float16 *pb0, *pb1;  // PREC 3: P0 / P1 at (column cl, k 8g)
     const int *ecol;          // PREC 3: scale exponent of each IN column
-    ECol ecl;                 // PREC 3: this lane's columns' exponents from the wave's last publish
+    int ecl[CT];              // PREC 3: this lane's columns' exponents from the wave's last publish
     Fair fair;                // PREC 3 forward: pipe sharing with the SIMD-mate (fair.prog NULL: off)
     int wave, lane;
 #ifdef PNR_PHASE_TIMING
@@ -1023,64 +875,11 @@ struct GemmCtx {
 // LDS as fp32 stage[column][LDS_LD]: resnetfc.py:160-163 on grid_sample's blend
 // (encoder.py:102-108), evaluated by linearity as the blend of four rows of the projected
 // latent P = latent W_z^T (proj.hip), torch's nw, ne, sw, se summation order.  Wave w blends
-// the COLS / WAVES columns [8w, 8w + 8), in two batches of 4; each load instruction reads one
-// contiguous 1 KB half of a corner's 2 KB row.  The stage aliases the GEMM input image, so
-// the first batch's loads are issued BEFORE the barrier that frees it (proj_load) and land
-// while the wave waits for its SIMD-mate's GEMM; blends and LDS writes come after.
-#ifndef PNR_PJ
-#define PNR_PJ 4
-#endif
-constexpr int PJ = PNR_PJ;                // columns in the batch loaded before the barrier
-constexpr int PJ2 = COLS / WAVES - PJ;    // the rest, loaded after it
-template <int N>
-struct ProjRows {
-    f4 c[N][2][4];      // [column][channel half][corner]
-    f4 tw[N];           // bilinear weights nw, ne, sw, se
-};
-template <int N>
-__device__ __forceinline__ void proj_load(ProjRows<N> &R, const float *__restrict__ pz, const float *gtab, int j0,
-                                          int wave, int lane) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        const int cj = (COLS / WAVES) * wave + j0 + j;
-        const f4 to = *reinterpret_cast<const f4 *>(gtab + cj * 8);
-        R.tw[j] = *reinterpret_cast<const f4 *>(gtab + cj * 8 + 4);
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
-#ifdef PNR_ABLATE_GATHER
-            R.c[j][half][0] = R.c[j][half][1] = R.c[j][half][2] = R.c[j][half][3] = to;   // diagnostic: no loads
-#else
-            R.c[j][half][0] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.x) + ch);
-            R.c[j][half][1] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.y) + ch);
-            R.c[j][half][2] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.z) + ch);
-            R.c[j][half][3] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.w) + ch);
-#endif
-        }
-    }
-}
-template <int N>
-__device__ __forceinline__ void proj_blend_store(const ProjRows<N> &R, float *stage, int j0, int wave, int lane) {
-#pragma unroll
-    for (int j = 0; j < N; ++j) {
-        const int cj = (COLS / WAVES) * wave + j0 + j;
-        const f4 tw = R.tw[j];
-#pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
-            const f4 *c = R.c[j][half];
-            f4 zz;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                zz[q] = add_rn(add_rn(add_rn(mul_rn(c[0][q], tw.x), mul_rn(c[1][q], tw.y)), mul_rn(c[2][q], tw.z)),
-                               mul_rn(c[3][q], tw.w));
-            *reinterpret_cast<f4 *>(stage + cj * LDS_LD + ch) = zz;
-        }
-    }
-}
-static_assert(PJ > 0 && PJ2 > 0, "two batches cover a wave's columns");
-
-// Run-deduplicated stage (PNR_PROJ_RUNS, the default).  A wave's 8 columns are consecutive
+// the COLS / WAVES columns [8w, 8w + 8); each load instruction reads one contiguous 1 KB half
+// of a corner's 2 KB row.  The stage aliases the GEMM input image, so the first loads are
+// issued BEFORE the barrier that frees it and land while the wave waits for its SIMD-mate's
+// GEMM; blends and LDS writes come after.
+// The stage is run-deduplicated.  A wave's 8 columns are consecutive
 // samples of one ray, and consecutive samples mostly project into the same latent cell
 // (cfg3: 2.1 runs of equal cell per 8 columns, cfg2: 4.9): the 4 corner rows of a run are
 // loaded ONCE and blended with each of its columns' weights (the blend arithmetic per column
@@ -1088,9 +887,6 @@ static_assert(PJ > 0 && PJ2 > 0, "two batches cover a wave's columns");
 // the runs: runs 0-2 are issued before the barrier that frees the stage, run k + 3 as soon
 // as run k's columns are blended.  The run pattern is wave-uniform (SGPR bit mask), so every
 // branch below is a scalar branch.
-#ifndef PNR_PROJ_RUNS
-#define PNR_PROJ_RUNS 1
-#endif
 struct CellRows {
     f4 c[2][4];   // [channel half][corner nw, ne, sw, se]
 };
@@ -1100,10 +896,14 @@ __device__ __forceinline__ void cell_load(CellRows &C, const float *__restrict__
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
         const uint32_t ch = half * 256 + opaque_lane(lane) * 4;
+#ifdef PNR_ABLATE_GATHER   // diagnostic (results invalid): no projected-row loads
+        C.c[half][0] = C.c[half][1] = C.c[half][2] = C.c[half][3] = to;
+#else
         C.c[half][0] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.x) + ch);
         C.c[half][1] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.y) + ch);
         C.c[half][2] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.z) + ch);
         C.c[half][3] = *reinterpret_cast<const f4 *>(pz + __float_as_uint(to.w) + ch);
+#endif
     }
 }
 __device__ __forceinline__ void cell_blend_store(const CellRows &C, const float *gtab, float *stage, int cj,
@@ -1191,10 +991,9 @@ __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, 
 
 // hidx: header slot of the layer's weight scale (0 lin_in, 1 + packed 512-wide index).
 // R: a ring primed (hring_prime) on this layer's weights, or nullptr (PREC 3 only).
-// EARLY (PREC 3, right after publish_relu, no barrier in between): the column exponents come
-// from the wave's own publish (g.ecl; ecol in LDS is not yet visible) and the GEMM starts on the
-// wave's own rows (gemm_f16_primed), so the barrier after the publish is inside the GEMM.
-template <int PREC, int NK, int DIST = H_DIST, bool EARLY = false>
+// OWN (PREC 3, the input image written by the wave's last publish): the column exponents come from
+// that publish's registers (g.ecl) instead of LDS, so the accumulator scaling does not wait on a read.
+template <int PREC, int NK, int DIST = H_DIST, bool OWN = false>
 __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx,
                                            HRing<DIST> *R = nullptr) {
     PT(g, 3);
@@ -1207,11 +1006,9 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         const int cl = opaque_lane(g.lane) & 15;
         const int ew = (int)g.hdr[HDR_ESCALE + hidx];
         float sa[CT], ia[CT];
-        int e_c[CT];
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-            const int e = (EARLY ? g.ecl.e[c] : g.ecol[16 * c + cl]) + ew;
-            e_c[c] = e;
+            const int e = (OWN ? g.ecl[c] : g.ecol[16 * c + cl]) + ew;
             sa[c] = __builtin_ldexpf(1.f, e);
             ia[c] = __builtin_ldexpf(1.f, -e);
         }
@@ -1219,27 +1016,16 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
-#if PNR_NO_PK   // one v_ldexp_f32 per value (exact, as the power-of-two multiply)
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[r][c][q] = __builtin_ldexpf(acc[r][c][q], e_c[c]);
-#else
                 acc[r][c] *= sa[c];
-#endif
             }
-        const int rot = EARLY ? 2 * g.wave : 0;
         Fair *F = g.fair.prog ? &g.fair : nullptr;
-        if (R) gemm_f16_primed<NK / 2, DIST, EARLY>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot, F);
-        else gemm_f16<NK / 2, DIST, EARLY>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, rot, F);
+        if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
+        else gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
 #pragma unroll
             for (int c = 0; c < CT; ++c) {
-#if PNR_NO_PK
-#pragma unroll
-                for (int q = 0; q < 4; ++q) acc[r][c][q] = __builtin_ldexpf(acc[r][c][q], -e_c[c]);
-#else
                 acc[r][c] *= ia[c];
-#endif
             }
     } else {
         gemm_split<NK / 2, PREC>(acc, layer_base + g.ws_off, g.inbw, g.stg, g.wave, g.lane);
@@ -1319,12 +1105,7 @@ __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const f
 // keeps its own register allocation
 template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
-    constexpr int KD = PZ ? H_DIST : H_DIST_3;   // weight ring distance
-    constexpr bool EG = PREC == 3 && kEarlyGemm;   // early GEMM start after the relu publishes
-    // PNR_SPREAD_PRIME (off: 0.5-1 % slower): the next GEMM's ring prime issued inside
-    // the publish's split, one row tile per column tile
-    // (the vector-memory path then works under the split's VALU instead of in a burst before it)
-    constexpr bool SP = PREC == 3 && PNR_SPREAD_PRIME && !EG && KD == CT;
+    constexpr int KD = H_DIST;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
     const int tid = threadIdx.x;
@@ -1359,12 +1140,11 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
     gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
-    for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
     gc.fair.prog = nullptr;
     gc.fair.wave = wave;
     gc.fair.it = 0;
     gc.fair.mate = 0;
-    if constexpr (PREC == 3 && PNR_FAIR && WAVES == 8) {
+    if constexpr (PREC == 3) {
         gc.fair.prog = reinterpret_cast<int *>(petab + 40);   // petab + 32 / 33: s_next, + 64: hpart
         if (tid < WAVES) gc.fair.prog[tid] = 0;   // visible after the first barrier
     }
@@ -1396,7 +1176,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
             lds_barrier();
     };
-    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0, auto pf) {
+    auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (a.save) {
             save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
             save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
@@ -1409,7 +1189,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #pragma unroll
                 for (int c = 0; c < CT; ++c) t += acc[r][c].x + acc[r][c].y + acc[r][c].z + acc[r][c].w;
             cmax[tid & 511] = t;
-            for (int c = 0; c < CT; ++c) pf(c);
+            for (int c = 0; c < CT; ++c) gc.ecl[c] = -8;
             return;
         }
 #endif
@@ -1421,7 +1201,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 13);
             lds_barrier();
             PT(gc, 14);
-            gc.ecl = relu_store_split(acc, P0, P1, cmax, ecol, wave, lane, pf);
+            relu_store_split(acc, P0, P1, cmax, ecol, wave, lane, gc.ecl);
             PT(gc, 15);
         } else {
             store_relu(acc, inbuf, wave, lane);
@@ -1456,21 +1236,12 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // march (m.single) its kpt_f fine tiles after them
     const bool single = MARCH && march_cfg(a)->single;
     const int upt = single ? kpt + march_cfg(a)->kpt_f : kpt;
-    // PNR_LOCKSTEP = E > 0 (diagnostic A/B): static per-XCD rounds instead --
-    // workgroup j of XCD x takes unit lo_x + r n_x + j in round r -- and every E rounds the
-    // XCD's workgroups meet at a spin barrier, so that they run the same layers at the same time
-    // and one layer's weight fragments serve all 32 CUs from the XCD's 4 MB L2.  The barrier is
-    // pacing only (no data crosses it): the spin is bounded (50 us) and a timed-out wait proceeds.
-    int lk_round = 0;   // tid 0: rounds taken
+    // single launch: the fine tiles' PE table from the fine pack's header (the packs
+    // of two MLPs may carry different tables); visible after the first barrier
+    float *petab_f = mnf + 4;
+    if (single && tid >= 64 && tid < 96) petab_f[tid - 64] = march_cfg(a)->packed_f[tid - 64];
     auto grab = [&]() -> int {
         const int64_t T = a.n_tiles / upt;
-        if constexpr (PNR_LOCKSTEP > 0) {
-            const int x = blockIdx.x & 7, nx = ((int)gridDim.x - x + 7) >> 3, j = blockIdx.x >> 3;
-            const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
-            const int64_t i = lo + (int64_t)lk_round * nx + j;
-            s_next[1] = lk_round++;
-            return i < hi ? (int)(i * upt) : (int)a.n_tiles;
-        }
         const int x0 = blockIdx.x & 7;
         for (int k = 0; k < 8; ++k) {
             const int x = (x0 + k) & 7;
@@ -1484,25 +1255,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     if (tid == 0) *s_next = grab();
     lds_barrier();
     for (int64_t tile = *s_next; tile < a.n_tiles; tile = *s_next) {
-        if constexpr (PNR_LOCKSTEP > 0) {
-            const int rnd = s_next[1];   // written with s_next, read after the same barrier
-            if (tile % upt == 0 && rnd > 0 && rnd % PNR_LOCKSTEP == 0) {
-                if (tid == 0) {
-                    const int x = blockIdx.x & 7, nx = ((int)gridDim.x - x + 7) >> 3;
-                    const int64_t T = a.n_tiles / upt, lo = x * T / 8, hi = (x + 1) * T / 8;
-                    const int64_t left = hi - lo - (int64_t)rnd * nx;   // units of this round
-                    const int part = left < nx ? (int)left : nx;
-                    const int target = (rnd / PNR_LOCKSTEP - 1) * nx + part;
-                    int *cnt = a.tile_ctr + 16 * x;
-                    __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-                    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-                           __builtin_amdgcn_s_memrealtime() - t0 < 5000)   // 100 MHz: 50 us
-                        __builtin_amdgcn_s_sleep(2);
-                }
-                lds_barrier();
-            }
-        }
         // this tile within its unit: pass_f = a fine tile of the single-launch march; sub = the
         // tile within its pass (the ray's kpt_t tiles of K_t = 64 kpt_t samples)
         const int64_t unit = tile / upt;
@@ -1590,6 +1342,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             }
             {
                 const int npe = 3 * L.pe_n;
+                const float *pet = MARCH && pass_f ? petab_f : petab;   // this pass's PE table
                 float fv[FPT];
 #pragma unroll
                 for (int i = 0; i < FPT; ++i) {
@@ -1599,7 +1352,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     else if (f < 3 + npe) {
                         const int m = f - 3, q = m / 3, d = m - 3 * q;
                         const float xd = d == 0 ? xr[0] : (d == 1 ? xr[1] : xr[2]);
-                        val = sinf(add_rn(petab[16 + q], mul_rn(xd, petab[q])));   // code._phases, _freqs
+                        val = sinf(add_rn(pet[16 + q], mul_rn(xd, pet[q])));   // code._phases, _freqs
                     } else if (f < 6 + npe) {
                         const int d = f - 3 - npe;
                         val = d == 0 ? vd[0] : (d == 1 ? vd[1] : vd[2]);
@@ -1679,19 +1432,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     // the stage aliases the image the previous GEMM read; publish_relu's
                     // internal barrier orders the add_stage reads before the image writes
                     const float *pz = PJ_() + blk * a.proj_stride;
-#if PNR_PROJ_RUNS && !defined(PNR_ABLATE_GATHER)
                     stage_proj_runs(pz, gtab, inbuf, wave, lane);
                     PT(gc, 3);
-#else
-                    ProjRows<PJ> rows;
-                    proj_load(rows, pz, gtab, 0, wave, lane);
-                    lds_barrier();
-                    PT(gc, 3);
-                    proj_blend_store(rows, inbuf, 0, wave, lane);
-                    ProjRows<PJ2> rows2;
-                    proj_load(rows2, pz, gtab, PJ, wave, lane);
-                    proj_blend_store(rows2, inbuf, PJ, wave, lane);
-#endif
                     lds_barrier();
                     PT(gc, 1);
                     add_bias(x, bias + (1 + lz) * H, wave, lane, true);
@@ -1755,32 +1497,26 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 }
                 HRing<KD> R0;   // fc_0's ring, primed before or during the publish (PREC 3)
                 const float *w0p = PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats;
-                if constexpr (PREC == 3 && !SP) hring_prime(R0, w0p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+                if constexpr (PREC == 3) hring_prime(R0, w0p + opaque_lane((int)gc.ws_off));
                 f4 nb0[RTW];   // fc_0's bias rows, loaded before the publish too
                 load_bias(nb0, bias + (2 + lz) * H, wave, lane);
-                publish_relu(x, tile, blk, v * P, [&](int t) {
-                    if constexpr (SP) hring_load(R0, w0p + opaque_lane((int)gc.ws_off), t, 0, t);
-                });
-                if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
-                if constexpr (!EG) lds_barrier();   // EG: inside the GEMM, after the wave's own rows
+                publish_relu(x, tile, blk, v * P);
+                lds_barrier();
                 PT(gc, 16);
                 set_bias(h, nb0, false);
-                layer_gemm<PREC, NKB, KD, EG>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
+                layer_gemm<PREC, NKB, KD, PREC == 3>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
                                           PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
                 const float *w1p = PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats;
-                if constexpr (PREC == 3 && !SP) hring_prime(R1, w1p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+                if constexpr (PREC == 3) hring_prime(R1, w1p + opaque_lane((int)gc.ws_off));
                 f4 nb1[RTW];
                 load_bias(nb1, bias + (3 + lz) * H, wave, lane);
-                publish_relu(h, tile, L.n_blocks + blk, v * P, [&](int t) {
-                    if constexpr (SP) hring_load(R1, w1p + opaque_lane((int)gc.ws_off), t, 0, t);
-                });
-                if constexpr (!EG) lds_barrier();
+                publish_relu(h, tile, L.n_blocks + blk, v * P);
+                lds_barrier();
                 PT(gc, 16);
-                if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
                 set_bias(x, nb1, true);
-                layer_gemm<PREC, NKB, KD, EG>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
+                layer_gemm<PREC, NKB, KD, PREC == 3>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
                                           PREC == 3 ? &R1 : nullptr);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
@@ -1818,38 +1554,32 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             pre_publish_sync();
             HRing<KD> R0;
             const float *w0p = PK() + L.off_l512 + (int64_t)l0 * L.layer_floats;
-            if constexpr (PREC == 3 && !SP) hring_prime(R0, w0p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+            if constexpr (PREC == 3) hring_prime(R0, w0p + opaque_lane((int)gc.ws_off));
             f4 nb0[RTW];
             load_bias(nb0, bias + (1 + l0) * H, wave, lane);
-            publish_relu(x, tile, blk, 0, [&](int t) {
-                if constexpr (SP) hring_load(R0, w0p + opaque_lane((int)gc.ws_off), t, 0, t);
-            });
-            if constexpr (PREC != 0 && kParkX) park(x, xp_ptr());
-            if constexpr (!EG) lds_barrier();
+            publish_relu(x, tile, blk, 0);
+            lds_barrier();
             PT(gc, 16);
             set_bias(h, nb0, false);
-            layer_gemm<PREC, NKB, KD, EG>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
+            layer_gemm<PREC, NKB, KD, PREC == 3>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
                                       PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
             HRing<KD> R1;
             const float *w1p = PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats;
-            if constexpr (PREC == 3 && !SP) hring_prime(R1, w1p + opaque_lane((int)gc.ws_off), EG ? 2 * wave : 0);
+            if constexpr (PREC == 3) hring_prime(R1, w1p + opaque_lane((int)gc.ws_off));
             f4 nb1[RTW];
             load_bias(nb1, bias + (2 + l0) * H, wave, lane);
-            publish_relu(h, tile, L.n_blocks + blk, 0, [&](int t) {
-                if constexpr (SP) hring_load(R1, w1p + opaque_lane((int)gc.ws_off), t, 0, t);
-            });
-            if constexpr (!EG) lds_barrier();
+            publish_relu(h, tile, L.n_blocks + blk, 0);
+            lds_barrier();
             PT(gc, 16);
-            if constexpr (PREC != 0 && kParkX) unpark(x, xp_ptr());
             set_bias(x, nb1, true);
-            layer_gemm<PREC, NKB, KD, EG>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
+            layer_gemm<PREC, NKB, KD, PREC == 3>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
                                       PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier
         pre_publish_sync();
-        publish_relu(x, tile, 2 * L.n_blocks, 0, [](int) {});
+        publish_relu(x, tile, 2 * L.n_blocks, 0);
         lds_barrier();
         PT(gc, 16);
         PT(gc, 3);
@@ -1904,7 +1634,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
                 r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
-                r.w = fmaxf(o.w, 0.f);
+                r.w = max_nc(o.w, 0.f);   // torch.relu: NaN stays NaN
                 if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
                 if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * (sub * COLS + 16 * wave + cl)) = r;
             }
@@ -1925,7 +1655,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
                 r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
-                r.w = fmaxf(o.w, 0.f);
+                r.w = max_nc(o.w, 0.f);   // torch.relu: NaN stays NaN
                 if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
                 if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * (sub * COLS + 16 * wave + cc)) = r;
             }
@@ -1937,9 +1667,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         }
     }
 #ifdef PNR_PHASE_TIMING
-#ifndef PNR_PT_WAVE
-#define PNR_PT_WAVE 0
-#endif
     if (threadIdx.x == 64 * PNR_PT_WAVE)   // the recorded wave
         for (int i = 0; i < PT_SLOTS; ++i) atomicAdd(&g_phase[i], (unsigned long long)gc.pt[i]);
 #endif
@@ -2079,12 +1806,11 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
     gc.pb1 = P1 + cl * ROWH + swz(cl, 8 * g);
     gc.ecol = ecol;
-    for (int c = 0; c < CT; ++c) gc.ecl.e[c] = 0;
     gc.fair.prog = nullptr;
     gc.fair.wave = wave;
     gc.fair.it = 0;
     gc.fair.mate = 0;
-    if constexpr (PNR_FAIR && WAVES == 8) {
+    {
         gc.fair.prog = ecol + COLS;   // 8 ints after ecol (the launch's LDS size counts them)
         if (threadIdx.x < WAVES) gc.fair.prog[threadIdx.x] = 0;
     }
@@ -2104,7 +1830,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
         // image after it, when every wave has left the GEMM that read the previous image
         relu_colmax<false>(acc, cmax, wave, lane);
         __syncthreads();
-        relu_store_split<false>(acc, P0, P1, cmax, ecol, wave, lane);
+        relu_store_split<false>(acc, P0, P1, cmax, ecol, wave, lane, gc.ecl);
         __syncthreads();
     };
     auto zero = [](Acc &acc) {
@@ -2170,13 +1896,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                 const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
                 zero(h);
                 load_mask(mk, mask_slot(nb + b, row0), tile, P, wave, lane);   // lands during the GEMM
-                layer_gemm<3, NKB, H_DIST_3>(h, layer(l1), gc, 1 + l1);
+                layer_gemm<3, NKB, H_DIST, true>(h, layer(l1), gc, 1 + l1);
                 relu_mask(h, mk, tile, P, lane);
                 store_rows(h, dy_slot(b, row0), tile, P, wave, lane, bs_slot(b), first);
                 publish(h);
                 zero(h);
                 load_mask(mk, mask_slot(b, row0), tile, P, wave, lane);
-                layer_gemm<3, NKB, H_DIST_3>(h, layer(l0), gc, 1 + l0);
+                layer_gemm<3, NKB, H_DIST, true>(h, layer(l0), gc, 1 + l0);
                 relu_mask(h, mk, tile, P, lane);
 #pragma unroll
                 for (int r = 0; r < RTW; ++r)
@@ -2188,7 +1914,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                     published = true;
                     const int lz = layer_index(b, 0, L.n_linz);
                     zero(h);
-                    layer_gemm<3, NKB, H_DIST_3>(h, layer(lz), gc, 1 + lz);
+                    layer_gemm<3, NKB, H_DIST, true>(h, layer(lz), gc, 1 + lz);
                     const bool zfirst = b == L.n_linz - 1;
 #pragma unroll
                     for (int c = 0; c < CT; ++c) {

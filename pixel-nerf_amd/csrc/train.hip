@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
         const bool valid = k < K;
         const float zn = k + 1 >= K ? far : (i + 1 < S ? zk[i + 1] : z_next_lane);
         delta[i] = sub_rn(zn, zk[i]);
-        sg[i] = fmaxf(v[i].w, 0.0f);
+        sg[i] = max_nc(v[i].w, 0.0f);
         ex[i] = expf(mul_rn(-delta[i], sg[i]));
         alpha[i] = valid ? sub_rn(1.0f, ex[i]) : 0.0f;
         const float shifted = valid ? add_rn(sub_rn(1.0f, alpha[i]), 1e-10f) : 1.0f;

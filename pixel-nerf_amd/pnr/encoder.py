@@ -19,7 +19,7 @@ from torch import nn
 
 from .consts import device_const
 
-__all__ = ["SpatialEncoder", "resnet34_trunk"]
+__all__ = ["SpatialEncoder", "ImageEncoder", "resnet34_trunk"]
 
 
 def _latent_channels_last(maps):
@@ -144,8 +144,9 @@ class SpatialEncoder(nn.Module):
         super().__init__()
         if backbone != "resnet34":
             raise NotImplementedError("pnr SpatialEncoder implements backbone=resnet34 only")
-        if index_interp != "bilinear" or index_padding != "border":
-            raise NotImplementedError("the HIP gather implements bilinear / border indexing")
+        # index_interp / index_padding other than bilinear / border: the fused kernel's gather
+        # does not implement them, so such models take the callback path (F.grid_sample in
+        # index(), PixelNeRFNet.fused_conf_reason)
         self.feature_scale = feature_scale
         self.use_first_pool = use_first_pool
         self.model = resnet34_trunk(pretrained, _norm_layer(norm_type))
@@ -237,3 +238,41 @@ class SpatialEncoder(nn.Module):
                    upsample_interp=conf.get_string("upsample_interp", "bilinear"),
                    feature_scale=conf.get_float("feature_scale", 1.0),
                    use_first_pool=conf.get_bool("use_first_pool", True))
+
+
+class ImageEncoder(nn.Module):
+    """Global image encoder (encoder.py:180-240): the ResNet34 trunk through layer4 and a global
+    average pool, then ``fc`` to ``latent_size`` when that is not 512.  Its latent (B, L) is
+    concatenated to every point's MLP input (models.py:229-235); models using it take the
+    callback path (PixelNeRFNet.fused_conf_reason)."""
+
+    def __init__(self, backbone="resnet34", pretrained=True, latent_size=128):
+        super().__init__()
+        if backbone != "resnet34":
+            raise NotImplementedError("pnr ImageEncoder implements backbone=resnet34 only")
+        self.model = resnet34_trunk(pretrained)
+        self.model.avgpool = nn.AdaptiveAvgPool2d((1, 1))   # torchvision's; fc replaced as the reference does
+        self.register_buffer("latent", torch.empty(1, 1), persistent=False)
+        self.latent_size = latent_size
+        if latent_size != 512:
+            self.fc = nn.Linear(512, latent_size)
+
+    def index(self, uv, cam_z=None, image_size=(), z_bounds=()):
+        """(B, L, N): the global latent for each of uv's N points (uv only gives the shape)."""
+        return self.latent.unsqueeze(-1).expand(-1, -1, uv.shape[1])
+
+    def forward(self, x):
+        x = x.to(device=self.latent.device)
+        m = self.model
+        x = m.maxpool(m.relu(m.bn1(m.conv1(x))))
+        x = m.layer4(m.layer3(m.layer2(m.layer1(x))))
+        x = torch.flatten(m.avgpool(x), 1)
+        if self.latent_size != 512:
+            x = self.fc(x)
+        self.latent = x
+        return self.latent
+
+    @classmethod
+    def from_conf(cls, conf):
+        return cls(conf.get_string("backbone"), pretrained=conf.get_bool("pretrained", True),
+                   latent_size=conf.get_int("latent_size", 128))

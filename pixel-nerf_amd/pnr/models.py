@@ -7,6 +7,13 @@ unchanged.  The per-point evaluation (``forward``, models.py:146-266) and the
 full ray march (``pnr.renderer.NeRFRenderer``) run in libpnr.so on the HIP
 device; the nn.Linear modules here are the parameter store the kernels read
 (packed once per weight version by ``pnr_mlp_pack``).
+
+Confs the fused kernel does not implement (``PixelNeRFNet.fused_conf_reason()``: softplus
+``beta``, widths other than 512, ``use_code_viewdirs``, SPADE, max-combine, the global encoder,
+other grid_sample modes) take the reference's callback path instead: the model
+runs as device torch ops (``PixelNeRFNet.forward`` -> ``ResnetFC.forward``, hipBLASLt GEMMs)
+and NeRFRenderer still samples and composites on the HIP kernels.  CPU tensors are refused on
+both paths.
 """
 import os
 import os.path as osp
@@ -20,7 +27,8 @@ from torch import nn
 from . import _lib
 from .consts import device_const
 from .conf import as_conf
-from .encoder import SpatialEncoder
+from .encoder import ImageEncoder, SpatialEncoder
+from .util import combine_interleaved, repeat_interleave
 
 __all__ = ["PositionalEncoding", "ResnetBlockFC", "ResnetFC", "PixelNeRFNet", "make_model",
            "make_mlp", "make_encoder", "PRECISIONS"]
@@ -91,7 +99,8 @@ class PositionalEncoding(nn.Module):
 
 
 class ResnetBlockFC(nn.Module):
-    """x + fc_1(relu(fc_0(relu(x)))) (resnetfc.py:10-62); parameters only."""
+    """x + fc_1(act(fc_0(act(x)))), act = relu or softplus(beta) (resnetfc.py:10-62).  The
+    fused kernel reads the parameters; ``forward`` is the callback path's device evaluation."""
 
     def __init__(self, size_in, size_out=None, size_h=None, beta=0.0):
         super().__init__()
@@ -105,13 +114,20 @@ class ResnetBlockFC(nn.Module):
         nn.init.constant_(self.fc_1.bias, 0.0)
         nn.init.zeros_(self.fc_1.weight)
         self.beta = beta
+        self.activation = nn.Softplus(beta=beta) if beta > 0 else nn.ReLU()
         self.shortcut = None
         if size_in != size_out:
             self.shortcut = nn.Linear(size_in, size_out, bias=False)
 
+    def forward(self, x):
+        h = self.fc_0(self.activation(x))
+        res = x if self.shortcut is None else self.shortcut(x)
+        return res + self.fc_1(self.activation(h))
+
 
 class ResnetFC(nn.Module):
-    """ResnetFC parameter layout (resnetfc.py:65-198)."""
+    """ResnetFC (resnetfc.py:65-198): the parameter layout the fused kernel reads, and the
+    callback path's device forward for confs the kernel does not implement."""
 
     def __init__(self, d_in, d_out=4, n_blocks=5, d_latent=0, d_hidden=128, beta=0.0,
                  combine_layer=1000, combine_type="average", use_spade=False):
@@ -128,6 +144,7 @@ class ResnetFC(nn.Module):
         self.combine_layer, self.combine_type, self.use_spade = combine_layer, combine_type, use_spade
         self.beta = beta
         self.blocks = nn.ModuleList([ResnetBlockFC(d_hidden, beta=beta) for _ in range(n_blocks)])
+        self.activation = nn.Softplus(beta=beta) if beta > 0 else nn.ReLU()
         if d_latent != 0:
             n_lin_z = min(combine_layer, n_blocks)
             self.lin_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
@@ -137,9 +154,21 @@ class ResnetFC(nn.Module):
             if use_spade:
                 self.scale_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("ResnetFC is evaluated inside the fused HIP kernel; call "
-                                  "PixelNeRFNet.forward or NeRFRenderer instead")
+    def forward(self, zx, combine_inner_dims=(1,), combine_index=None, dim_size=None):
+        """(N, d_latent + d_in) -> (N', d_out) (resnetfc.py:132-184), as device torch ops: the
+        callback path of PixelNeRFNet confs the fused kernel does not implement (the fused
+        kernel evaluates the shipped conf inside the ray march).  ``combine_index`` /
+        ``dim_size`` are the reference's disabled frustum-culling arguments (ignored there)."""
+        z, x = zx[..., :self.d_latent], zx[..., self.d_latent:]
+        x = self.lin_in(x) if self.d_in > 0 else torch.zeros(self.d_hidden, device=zx.device)
+        for b, blk in enumerate(self.blocks):
+            if b == self.combine_layer:
+                x = combine_interleaved(x, combine_inner_dims, self.combine_type)
+            if self.d_latent > 0 and b < self.combine_layer:
+                t = self.lin_z[b](z)
+                x = self.scale_z[b](z) * x + t if self.use_spade else x + t
+            x = blk(x)
+        return self.lin_out(self.activation(x))
 
     @classmethod
     def from_conf(cls, conf, d_in, **kwargs):
@@ -333,7 +362,10 @@ class PixelNeRFNet(nn.Module):
         if self.use_viewdirs and not self.use_code_viewdirs:
             d_in += 3
         if self.use_global_encoder:
-            raise NotImplementedError("use_global_encoder is not implemented by the HIP path")
+            # global image feature (models.py:62-66); the model then takes the callback path
+            self.global_encoder = ImageEncoder.from_conf(conf["global_encoder"])
+            self.global_latent_size = self.global_encoder.latent_size
+            d_latent += self.global_latent_size
         d_out = 4
         self.latent_size = self.encoder.latent_size
         self.mlp_coarse = make_mlp(conf["mlp_coarse"], d_in, d_latent, d_out=d_out)
@@ -372,10 +404,13 @@ class PixelNeRFNet(nn.Module):
             self.num_views_per_obj = 1
         self.encoder(images)
         self._set_cameras(poses, focal, c, images.shape[-1], images.shape[-2])
+        if self.use_global_encoder:
+            self.global_encoder(images)
 
-    def encode_latent(self, latent, poses, focal, image_size, c=None, num_objs=1):
+    def encode_latent(self, latent, poses, focal, image_size, c=None, num_objs=1, global_latent=None):
         """Install a precomputed feature map (SB*NS, C, H_l, W_l) instead of running the
-        CNN; ``image_size`` = (W, H) of the source images."""
+        CNN; ``image_size`` = (W, H) of the source images.  ``global_latent`` (SB*NS, L): the
+        global encoder's output (use_global_encoder), likewise precomputed."""
         ns = latent.shape[0] // num_objs
         self.num_objs = num_objs
         self.num_views_per_obj = ns
@@ -383,6 +418,10 @@ class PixelNeRFNet(nn.Module):
             poses = poses.reshape(-1, 4, 4)
         self.encoder.set_latent(latent.float().contiguous())
         self._set_cameras(poses, focal, c, image_size[0], image_size[1])
+        if self.use_global_encoder:
+            if global_latent is None:
+                raise ValueError("use_global_encoder: pass the global latent (SB*NS, %d)" % self.global_latent_size)
+            self.global_encoder.latent = global_latent.float()
 
     def _set_cameras(self, poses, focal, c, width, height):
         dev = self.encoder.latent.device
@@ -432,18 +471,32 @@ class PixelNeRFNet(nn.Module):
                               dim=1).float().contiguous()
 
     # ---- HIP scene ------------------------------------------------------------------
-    def hip_unsupported_reason(self):
+    def fused_conf_reason(self):
+        """Why the fused HIP kernel cannot evaluate this model's CONFIGURATION (None: it can).
+        Such a model takes the reference's callback path: device torch ops for
+        the model, HIP kernels for sampling and compositing."""
         if not (self.use_encoder and self.use_xyz and self.normalize_z and self.use_code
                 and self.use_viewdirs and not self.use_code_viewdirs):
             return ("the fused kernel implements use_encoder, use_xyz, normalize_z, use_code, "
                     "use_viewdirs with use_code_viewdirs = False (the shipped confs)")
+        if self.use_global_encoder:
+            return "use_global_encoder"
         if self.code is None or not self.code.include_input:
             return "positional encoding must include the input"
+        if self.encoder.index_interp != "bilinear" or self.encoder.index_padding != "border":
+            return "the fused gather implements bilinear / border indexing"
         for mlp in (self.mlp_coarse, self.mlp_fine):
             if mlp is not None:
                 r = mlp.hip_unsupported_reason()
                 if r:
                     return r
+        return None
+
+    def hip_unsupported_reason(self):
+        """fused_conf_reason(), or a scene the fused path cannot render yet."""
+        r = self.fused_conf_reason()
+        if r:
+            return r
         if self.encoder.latent_cl.numel() == 0:
             return "encode() has not been called"
         if self.num_views_per_obj > 1 and self.mlp_coarse.combine_layer >= self.mlp_coarse.n_blocks:
@@ -503,7 +556,10 @@ class PixelNeRFNet(nn.Module):
     # ---- forward (point query) -----------------------------------------------------
     def forward(self, xyz, coarse=True, viewdirs=None, far=False):
         """(SB, B, 3) world points -> (SB, B, 4) [sigmoid(rgb), relu(sigma)]
-        (models.py:146-266) on the HIP device."""
+        (models.py:146-266) on the HIP device: the fused kernel for the confs it implements,
+        device torch ops (the callback path) for the others."""
+        if self.fused_conf_reason() is not None:
+            return self._forward_torch(xyz, coarse, viewdirs)
         self._require_hip()
         SB, B, _ = xyz.shape
         if SB != self.num_objs:
@@ -518,6 +574,49 @@ class PixelNeRFNet(nn.Module):
         proj = self.hip_proj(coarse)
         return torchops.load().point_query(*torchops.scene_args(self), torchops.desc_list(desc), packed, proj,
                                            xyz, vd)
+
+    def _forward_torch(self, xyz, coarse, viewdirs):
+        """models.py:146-266 as device torch ops (hipBLASLt GEMMs, grid_sample): the callback
+        path of confs the fused kernel does not implement.  Differentiable (training through
+        NeRFRenderer's callback path).  CPU tensors are refused as on the fused path."""
+        if xyz.device.type != "cuda":
+            raise ValueError("pnr: xyz must be on a HIP device (got %s); the HIP path has no CPU "
+                             "fallback" % xyz.device)
+        SB, B, _ = xyz.shape
+        NS = self.num_views_per_obj
+        rot = self.poses[:, None, :3, :3]
+        xyz = repeat_interleave(xyz, NS)                          # (SB NS, B, 3)
+        xyz_rot = torch.matmul(rot, xyz.unsqueeze(-1))[..., 0]
+        xyz = xyz_rot + self.poses[:, None, :3, 3]
+        feats = None
+        if self.d_in > 0:
+            p = xyz_rot if self.normalize_z else xyz
+            feats = p.reshape(-1, 3) if self.use_xyz else -p[..., 2].reshape(-1, 1)
+            if self.use_code and not self.use_code_viewdirs:
+                feats = self.code(feats)
+            if self.use_viewdirs:
+                assert viewdirs is not None
+                vd = repeat_interleave(viewdirs.reshape(SB, B, 3, 1), NS)
+                feats = torch.cat((feats, torch.matmul(rot, vd).reshape(-1, 3)), dim=1)
+            if self.use_code and self.use_code_viewdirs:
+                feats = self.code(feats)
+        mlp_input = feats
+        if self.use_encoder:
+            uv = -xyz[:, :, :2] / xyz[:, :, 2:]
+            uv = uv * repeat_interleave(self.focal.unsqueeze(1), NS if self.focal.shape[0] > 1 else 1)
+            uv = uv + repeat_interleave(self.c.unsqueeze(1), NS if self.c.shape[0] > 1 else 1)
+            lat = self.encoder.index(uv, None, self.image_shape)     # (SB NS, C, B)
+            if self.stop_encoder_grad:
+                lat = lat.detach()
+            lat = lat.transpose(1, 2).reshape(-1, self.latent_size)
+            mlp_input = lat if feats is None else torch.cat((lat, feats), dim=-1)
+        if self.use_global_encoder:
+            gl = self.global_encoder.latent
+            gl = repeat_interleave(gl, mlp_input.shape[0] // gl.shape[0])
+            mlp_input = torch.cat((gl, mlp_input), dim=-1)
+        mlp = self.mlp_coarse if (coarse or self.mlp_fine is None) else self.mlp_fine
+        out = mlp(mlp_input, combine_inner_dims=(NS, B)).reshape(-1, B, self.d_out)
+        return torch.cat((torch.sigmoid(out[..., :3]), torch.relu(out[..., 3:4])), dim=-1).reshape(SB, B, -1)
 
     # ---- checkpoints (models.py:268-316) -------------------------------------------
     def load_weights(self, args, opt_init=False, strict=True, device=None):

@@ -1,11 +1,13 @@
 """NeRFRenderer with the reference's interface (src/render/nerf.py:15-371).
 
 ``NeRFRenderer.forward(model, rays, want_weights)`` keeps the reference's
-contract.  When ``model`` is a :class:`pnr.models.PixelNeRFNet` the whole coarse
-+ fine march (sampling, fused point MLP, compositing, inverse-CDF resampling)
-runs as one stream-ordered sequence in libpnr.so (``pnr_render_forward``).  Any
-other model goes through the reference's plug point ``model(points, coarse,
-viewdirs)`` with sampling and compositing still on the HIP kernels.
+contract.  When ``model`` is a :class:`pnr.models.PixelNeRFNet` whose conf the fused
+kernel implements, the whole coarse + fine march (sampling, fused point MLP,
+compositing, inverse-CDF resampling) runs as one stream-ordered sequence in libpnr.so
+(``pnr_render_forward``).  Any other model -- including a PixelNeRFNet with a conf the
+kernel does not implement (``fused_conf_reason()``) -- goes through the reference's plug
+point ``model(points, coarse, viewdirs)`` with sampling and compositing still on the HIP
+kernels, and with autograd when gradients are on.
 
 Random draws (nerf.py:111, 135, 141, 158), ``rng_mode``:
   "counter" (default on the fused path) -- the kernels draw on device from a
@@ -151,10 +153,15 @@ class NeRFRenderer(torch.nn.Module):
             for pts in torch.split(points, ebs, dim=dim):
                 vals.append(model(pts, coarse=coarse))
         out = torch.cat(vals, dim=dim).reshape(B, K, -1)
-        if self.training and self.noise_std > 0.0:
-            out = out.clone()
-            out[..., 3] = out[..., 3] + torch.randn_like(out[..., 3]) * self.noise_std
-        return ops.composite(z_samp, out[..., :4].contiguous(), rays, self.white_bkgd)
+        if self.training and self.noise_std > 0.0:   # nerf.py:225-226 (sigma only)
+            n = torch.randn_like(out[..., 3])
+            out = torch.cat([out[..., :3], out[..., 3:4] + (n * self.noise_std).unsqueeze(-1), out[..., 4:]], -1)
+        raw = out[..., :4].contiguous()
+        if torch.is_grad_enabled() and (raw.requires_grad or z_samp.requires_grad):
+            from .train import Composite   # the composite kernel with its backward kernel
+
+            return Composite.apply(z_samp, raw, rays, self.white_bkgd)
+        return ops.composite(z_samp, raw, rays, self.white_bkgd)
 
     # ---- forward (nerf.py:251-303) ---------------------------------------------------
     def forward(self, model, rays, want_weights=False):
@@ -167,7 +174,7 @@ class NeRFRenderer(torch.nn.Module):
         B = rays.shape[0]
         from .models import PixelNeRFNet
 
-        if isinstance(model, PixelNeRFNet):
+        if isinstance(model, PixelNeRFNet) and model.fused_conf_reason() is None:
             # the sigma noise of training mode (nerf.py:225-226) is added between the model
             # and the composite, which the fused march does not expose: the training
             # graph's kernels run it, with or without autograd
@@ -177,7 +184,7 @@ class NeRFRenderer(torch.nn.Module):
             if self.streams is None and self.rng_mode == "counter":
                 return self._forward_fused(model, rays, sb, None, want_weights)
             return self._forward_fused(model, rays, sb, self.draw_streams(B, rays.device), want_weights)
-        return self._forward_callback(model, rays, sb, self.draw_streams(B, rays.device), want_weights)
+        return self._forward_callback(model, rays, sb, want_weights)
 
     def _forward_train(self, net, rays, sb, want_weights):
         """The reference's autograd graph (nerf.py:251-303) over the HIP kernels
@@ -313,15 +320,40 @@ class NeRFRenderer(torch.nn.Module):
                                           z_f if self.return_z else None)
         return outputs
 
-    def _forward_callback(self, model, rays, sb, streams, want_weights):
-        u_c, u_f, u_j, n_d = streams
+    def _forward_callback(self, model, rays, sb, want_weights):
+        """nerf.py:251-303 through the plug point ``model(points, coarse, viewdirs)``; sampling
+        and compositing on the HIP kernels.  Under autograd the depth samples keep their
+        gradient to the coarse depth (nerf.py:150-161, 292) and the fine depths are sorted with
+        torch.sort, as in the reference's graph.  With training-mode sigma noise the draws
+        interleave with the noise draws in the reference's order."""
+        B, dev = rays.shape[0], rays.device
+        nf, kfd = self.fine_counts()
+        lazy = self.training and self.noise_std > 0.0 and self.streams is None
+        if lazy:
+            u_c = torch.rand(B, self.n_coarse, device=dev)
+        else:
+            u_c, u_f, u_j, n_d = self.draw_streams(B, dev)
         z_c = self.sample_coarse(rays, u_c)
         w_c, rgb_c, depth_c = self.composite(model, rays, z_c, coarse=True, sb=sb)
         outputs = DotMap(coarse=self._pack_out(w_c, rgb_c, depth_c, sb, want_weights, z_c))
         if self.using_fine:
-            nf, kfd = self.fine_counts()
-            z_f = z_c if nf + kfd == 0 else ops.sample_fine(rays, z_c, w_c.detach(), depth_c, nf + kfd, kfd,
-                                                            self.depth_std, u_f, u_j, n_d, self.lindisp)
+            if lazy:
+                empty = torch.zeros(B, 0, device=dev)
+                u_f = torch.rand(B, nf, device=dev) if nf > 0 else empty
+                u_j = torch.rand(B, nf, device=dev) if nf > 0 else empty
+                n_d = torch.randn(B, kfd, device=dev) if kfd > 0 else empty
+            if nf + kfd == 0:
+                z_f = z_c
+            elif torch.is_grad_enabled() and kfd > 0 and depth_c.requires_grad:
+                with torch.no_grad():
+                    z_ci = (ops.sample_fine(rays, z_c, w_c.detach(), depth_c.detach(), nf, 0, self.depth_std, u_f,
+                                            u_j, None, self.lindisp) if nf > 0 else z_c)
+                z_d = depth_c.unsqueeze(1).repeat((1, kfd)) + n_d * self.depth_std
+                z_d = torch.max(torch.min(z_d, rays[:, -1:]), rays[:, -2:-1])
+                z_f = torch.sort(torch.cat([z_ci, z_d], -1), -1)[0].contiguous()
+            else:
+                z_f = ops.sample_fine(rays, z_c, w_c.detach(), depth_c.detach(), nf + kfd, kfd, self.depth_std,
+                                      u_f, u_j, n_d, self.lindisp)
             w_f, rgb_f, depth_f = self.composite(model, rays, z_f, coarse=False, sb=sb)
             outputs.fine = self._pack_out(w_f, rgb_f, depth_f, sb, want_weights, z_f)
         return outputs

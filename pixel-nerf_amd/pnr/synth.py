@@ -62,8 +62,9 @@ def _linear(seed, d_out, d_in):
 
 
 def resnetfc_state(seed, d_in=42, d_latent=512, d_hidden=512, n_blocks=5,
-                   combine_layer=3, d_out=4, prefix=""):
-    """State dict of a ResnetFC (resnetfc.py:65-130) with hash-init weights."""
+                   combine_layer=3, d_out=4, prefix="", use_spade=False):
+    """State dict of a ResnetFC (resnetfc.py:65-130) with hash-init weights (scale_z too with
+    use_spade, after every other layer so the other layers' seeds do not move)."""
     sd = {}
     k = 0
 
@@ -82,6 +83,9 @@ def resnetfc_state(seed, d_in=42, d_latent=512, d_hidden=512, n_blocks=5,
     if d_latent > 0:
         for i in range(min(combine_layer, n_blocks)):
             put("lin_z.%d" % i, d_hidden, d_latent)
+        if use_spade:
+            for i in range(min(combine_layer, n_blocks)):
+                put("scale_z.%d" % i, d_hidden, d_latent)
     return sd
 
 
@@ -95,17 +99,17 @@ def pe_buffers(num_freqs=6, freq_factor=1.5):
 
 
 def pixelnerf_state(seed, d_in=42, d_latent=512, d_hidden=512, n_blocks=5,
-                    combine_layer=3, with_fine=True, num_freqs=6, freq_factor=1.5):
+                    combine_layer=3, with_fine=True, num_freqs=6, freq_factor=1.5, use_spade=False):
     """Non-encoder part of a PixelNeRFNet state dict (62 keys)."""
     sd = {}
     f, ph = pe_buffers(num_freqs, freq_factor)
     sd["code._freqs"] = f
     sd["code._phases"] = ph
     sd.update(resnetfc_state(seed, d_in, d_latent, d_hidden, n_blocks, combine_layer,
-                             prefix="mlp_coarse."))
+                             prefix="mlp_coarse.", use_spade=use_spade))
     if with_fine:
         sd.update(resnetfc_state(seed + 1, d_in, d_latent, d_hidden, n_blocks,
-                                 combine_layer, prefix="mlp_fine."))
+                                 combine_layer, prefix="mlp_fine.", use_spade=use_spade))
     return sd
 
 

@@ -35,6 +35,26 @@ from . import _lib, ops
 
 __all__ = ["RenderPoints", "Composite", "mlp_backward", "mlp_backward_fused", "weight_grad", "mlp_params"]
 
+# Measurement hook (bench.py train leg): None, or {kernel: [(start, end, flop)]} -- HIP events
+# recorded on the launch stream around the training MLP kernels (torch's current stream, the one
+# every ctypes launch here uses) with each launch's algorithmic FLOP.  No host synchronization.
+KERNEL_EVENTS = None
+
+
+def _ev_begin():
+    if KERNEL_EVENTS is None:
+        return None
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
+def _ev_end(name, e0, flop):
+    if e0 is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        KERNEL_EVENTS.setdefault(name, []).append((e0, e1, float(flop)))
+
 
 def mlp_params(mlp):
     """The ResnetFC parameters in registration order (what autograd tracks), also on an
@@ -50,6 +70,29 @@ def _on_device(dev, what, *tensors):
     for name, t in zip(what.split(), tensors):
         if t is not None and t.device != dev:
             raise ValueError("pnr: %s is on %s, the launch device is %s" % (name, t.device, dev))
+
+
+def forward_flop(mlp, P, ns=1):
+    """Algorithmic FLOP of the ResnetFC forward over P points with ns source views (the reference's
+    per-point arithmetic, resnetfc.py:132-184: lin_in, lin_z and both block layers before
+    combine_layer once per view, the rest once per point, lin_out)."""
+    nb = mlp.n_blocks
+    nc = min(mlp.combine_layer, nb) if ns > 1 else nb
+    nz = len(getattr(mlp, "lin_z", []))
+    H, d_in = 512, mlp.lin_in.weight.shape[1]
+    per_view = 2 * H * d_in + 2 * H * H * (nz + 2 * nc)
+    per_point = 2 * H * H * 2 * (nb - nc) + 2 * 4 * H
+    return float(P) * (ns * per_view + per_point)
+
+
+def backward_chain_flop(mlp, P, ns=1):
+    """Algorithmic FLOP of k_mlp_bwd's input-gradient chain: W^T dY of every 512-wide layer (the
+    blocks before combine_layer once per view) and d_o W_out; lin_in's d_feat is a torch GEMM."""
+    nb = mlp.n_blocks
+    nc = min(mlp.combine_layer, nb) if ns > 1 else nb
+    nz = len(getattr(mlp, "lin_z", []))
+    H = 512
+    return float(P) * (ns * 2 * H * H * (nz + 2 * nc) + 2 * H * H * 2 * (nb - nc) + 2 * 4 * H)
 
 
 def _save_views(save, P, n_blocks, H=512, ns=1):
@@ -154,8 +197,10 @@ def weight_grad(dys, xs, P, arith="f16x3"):
         return (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])
 
     outs = (ctypes.c_void_p * n)(*[out[i].data_ptr() for i in range(n)])
+    e0 = _ev_begin()
     _lib.check(lib.pnr_weight_grad_arith(arr(dys), arr(xs), outs, n, P, _lib.WGRAD_ARITH[arith], _lib.ptr(ws),
                                          wsb, _lib.stream_of(dev)), "pnr_weight_grad_arith")
+    _ev_end("weight_grad", e0, 2.0 * 512 * 512 * n * P)
     return out
 
 
@@ -202,10 +247,12 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1, wgrad_arith="f1
     lib = _lib.load()
     wsb = lib.pnr_mlp_backward_workspace_bytes(desc, P)
     ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+    e0 = _ev_begin()
     _lib.check(lib.pnr_mlp_backward_views(desc, _lib.ptr(packed), _lib.ptr(packed_t), _lib.ptr(w_out),
                                           _lib.ptr(save), _lib.ptr(d_o), P, ns, _lib.ptr(dy), _lib.ptr(dzl),
                                           _lib.ptr(sums), _lib.ptr(ws), wsb, _lib.stream_of(dev)),
                "pnr_mlp_backward_views")
+    _ev_end("mlp_backward", e0, backward_chain_flop(mlp, P, ns))
     g = {}
     xf = slot(2 * nb, P)
     g[mlp.lin_out.weight] = _tall_mm(d_o, xf)
@@ -267,9 +314,11 @@ class RenderPoints(torch.autograd.Function):
         ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
         out = torch.empty(P, 4, dtype=torch.float32, device=dev)
         r = _lib.Rays(_lib.ptr(rays), B, B // net.num_objs)
+        e0 = _ev_begin()
         _lib.check(lib.pnr_render_points(sc, desc, _lib.ptr(packed), r, _lib.ptr(z), K, _lib.ptr(out),
                                          _lib.ptr(save), _lib.ptr(ws), ws_bytes, _lib.stream_of(dev)),
                    "pnr_render_points")
+        _ev_end("forward", e0, forward_flop(mlp, P, ns))
         ctx.save_for_backward(rays, z, out, save, latent_cl)
         ctx.net, ctx.mlp, ctx.desc, ctx.packed, ctx.params = net, mlp, desc, packed, params
         return out.view(B, K, 4)

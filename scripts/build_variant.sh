@@ -1,20 +1,26 @@
 #!/bin/bash
 # Build an A/B variant of libpnr.so into pixel-nerf_amd/build/<tag>/libpnr.so.
-#   scripts/build_variant.sh <tag> <git-rev|WORKTREE> [extra hipcc flags...]
-# The csrc/ sources come from <rev> (or the working tree); select the variant at run
-# time with PNR_LIB_PATH=pixel-nerf_amd/build/<tag>/libpnr.so (diagnostic only).
+#   [PATCH=tools/patches/<variant>.diff] scripts/build_variant.sh <tag> <git-rev|WORKTREE> [extra hipcc flags...]
+# The csrc/ sources come from <rev> (or the working tree), with PATCH (a rejected schedule variant,
+# tools/patches/) applied to the copy; the flags select diagnostics (csrc/pnr_diag.h) or the
+# patch's knob.  Select the variant at run time with PNR_LIB_PATH=pixel-nerf_amd/build/<tag>/libpnr.so
+# (diagnostic only).
 set -euo pipefail
 tag=$1; rev=$2; shift 2
 root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/pixel-nerf_amd/build/$tag
 src=$out/src
 rm -rf "$out"; mkdir -p "$src/csrc" "$src/include"
-for f in march.hip mlp.hip train.hip encoder.hip wgrad.hip proj.hip abi.cpp pnr_common.h march_dev.h; do
+for f in march.hip mlp.hip train.hip encoder.hip wgrad.hip proj.hip abi.cpp pnr_common.h march_dev.h pnr_diag.h; do
   if [ "$rev" = WORKTREE ]; then cp "$root/pixel-nerf_amd/csrc/$f" "$src/csrc/$f"
   else git -C "$root" show "$rev:pixel-nerf_amd/csrc/$f" > "$src/csrc/$f" 2>/dev/null || rm -f "$src/csrc/$f"; fi
 done
 if [ "$rev" = WORKTREE ]; then cp "$root/include/pnr_abi.h" "$src/include/"
 else git -C "$root" show "$rev:include/pnr_abi.h" > "$src/include/pnr_abi.h"; fi
+if [ -n "${PATCH:-}" ]; then
+  case $PATCH in /*) pf=$PATCH ;; *) pf=$root/$PATCH ;; esac
+  patch -s -p2 -d "$src" -i "$pf"
+fi
 # sources include "../../include/pnr_abi.h" relative to csrc/
 mkdir -p "$out/include"; cp "$src/include/pnr_abi.h" "$out/include/"
 objs=()

@@ -110,16 +110,30 @@ class Conf(dict):
         return self._get(k, default)
 
 
-def model_conf(d_hidden=512, num_layers=4, n_blocks=5, combine_layer=3):
+def model_conf(d_hidden=512, num_layers=4, n_blocks=5, combine_layer=3, opts=None):
+    """The shipped conf's model section; ``opts`` (the alt_* fixtures) sets the options the
+    fused kernel does not implement: beta, combine_type, use_spade, use_code_viewdirs,
+    index_padding / index_interp, global_latent_size (use_global_encoder)."""
+    o = dict(opts or {})
     mlp = dict(type="resnet", n_blocks=n_blocks, d_hidden=d_hidden,
-               combine_layer=combine_layer, combine_type="average")
-    return Conf(dict(
-        use_encoder=True, use_global_encoder=False, use_xyz=True, canon_xyz=False,
+               combine_layer=combine_layer, combine_type=o.get("combine_type", "average"),
+               beta=o.get("beta", 0.0), use_spade=o.get("use_spade", False))
+    enc = dict(backbone="resnet34", pretrained=False, num_layers=num_layers,
+               index_padding=o.get("index_padding", "border"), index_interp=o.get("index_interp", "bilinear"))
+    conf = dict(
+        use_encoder=True, use_global_encoder="global_latent_size" in o, use_xyz=True, canon_xyz=False,
         use_code=True, code=dict(num_freqs=6, freq_factor=1.5, include_input=True),
-        use_viewdirs=True, use_code_viewdirs=False,
-        mlp_coarse=dict(mlp), mlp_fine=dict(mlp),
-        encoder=dict(backbone="resnet34", pretrained=False, num_layers=num_layers),
-    ))
+        use_viewdirs=True, use_code_viewdirs=o.get("use_code_viewdirs", False),
+        mlp_coarse=dict(mlp), mlp_fine=dict(mlp), encoder=enc)
+    if "global_latent_size" in o:
+        conf["global_encoder"] = dict(backbone="resnet34", pretrained=False, latent_size=o["global_latent_size"])
+    return Conf(conf)
+
+
+def mlp_d_in(opts=None):
+    """ResnetFC d_in of model_conf (models.py:49-60): xyz PE 39 + raw viewdirs 3, or the PE of
+    (xyz, viewdirs) 6 + 72 with use_code_viewdirs."""
+    return 78 if (opts or {}).get("use_code_viewdirs") else 42
 
 
 @contextlib.contextmanager
@@ -157,20 +171,30 @@ def injected_rng(u_c, u_f, u_j, n_d):
 
 
 def build_reference_net(d_hidden, d_latent, seed, latent, poses, focal, c, width, height,
-                        n_blocks=5, combine_layer=3, with_fine=True):
+                        n_blocks=5, combine_layer=3, with_fine=True, opts=None, global_latent=None):
     from model import make_model  # reference src/model/__init__.py:4
 
     num_layers = {64: 1, 128: 2, 256: 3, 512: 4}[d_latent]
-    net = make_model(model_conf(d_hidden, num_layers, n_blocks, combine_layer))
+    o = opts or {}
+    net = make_model(model_conf(d_hidden, num_layers, n_blocks, combine_layer, o))
     if not with_fine:
         net.mlp_fine = None
-    sd = synth.pixelnerf_state(seed, d_latent=d_latent, d_hidden=d_hidden,
-                               n_blocks=n_blocks, combine_layer=combine_layer,
-                               with_fine=with_fine)
+    sd = synth.pixelnerf_state(seed, d_in=mlp_d_in(o), d_latent=d_latent + o.get("global_latent_size", 0),
+                               d_hidden=d_hidden, n_blocks=n_blocks, combine_layer=combine_layer,
+                               with_fine=with_fine, use_spade=o.get("use_spade", False))
     missing, unexpected = net.load_state_dict(sd, strict=False)
     assert not unexpected, unexpected
-    assert all(m.startswith("encoder.") for m in missing), missing
+    assert all(m.startswith("encoder.") or m.startswith("global_encoder.") for m in missing), missing
     enc = net.encoder
+    if global_latent is not None:
+        # what ImageEncoder.forward leaves behind (encoder.py:224-240): the latent is injected
+        ge = net.global_encoder
+
+        def fake_global(x):
+            ge.latent = global_latent.clone()
+            return ge.latent
+
+        ge.forward = fake_global
 
     def fake_forward(x):
         # what SpatialEncoder.forward leaves behind (encoder.py:160-164)
@@ -193,7 +217,8 @@ def build_reference_net(d_hidden, d_latent, seed, latent, poses, focal, c, width
 def render_case(name, *, d_hidden, d_latent, seed, scene, n_coarse, n_fine, n_fine_depth,
                 white_bkgd, lindisp=False, depth_std=0.01, sb=1, rng_seed=1,
                 want_weights=True, force_u_high=0, with_fine=True, n_blocks=5,
-                combine_layer=3, multi_obj_poses=None, focal_override=None, c_override=None):
+                combine_layer=3, multi_obj_poses=None, focal_override=None, c_override=None,
+                opts=None, global_latent=None):
     from render import NeRFRenderer  # reference src/render/__init__.py:1
 
     latent = scene["latent"]
@@ -202,7 +227,7 @@ def render_case(name, *, d_hidden, d_latent, seed, scene, n_coarse, n_fine, n_fi
     c = scene["c"] if c_override is None else c_override
     net = build_reference_net(d_hidden, d_latent, seed, latent, poses, focal, c,
                               scene["width"], scene["height"], n_blocks, combine_layer,
-                              with_fine)
+                              with_fine, opts, global_latent)
     renderer = NeRFRenderer(n_coarse=n_coarse, n_fine=n_fine, n_fine_depth=n_fine_depth,
                             depth_std=depth_std, white_bkgd=white_bkgd, lindisp=lindisp,
                             eval_batch_size=100000)
@@ -239,7 +264,7 @@ def render_case(name, *, d_hidden, d_latent, seed, scene, n_coarse, n_fine, n_fi
                height=scene["height"], near=scene["near"], far=scene["far"],
                latent_shape=list(latent.shape), rng_seed=rng_seed,
                force_u_high=force_u_high, with_fine=with_fine, n_blocks=n_blocks,
-               combine_layer=combine_layer, latent_seed=scene["latent_seed"])
+               combine_layer=combine_layer, latent_seed=scene["latent_seed"], opts=dict(opts or {}))
     arrays = dict(
         rays=rays3.numpy(), poses=poses.numpy(),
         focal=np.asarray(focal, dtype=np.float32),
@@ -249,6 +274,8 @@ def render_case(name, *, d_hidden, d_latent, seed, scene, n_coarse, n_fine, n_fi
         coarse_weights=out.coarse.weights.numpy(),
         z_coarse=captured["z"][0].numpy(),
     )
+    if global_latent is not None:
+        arrays["global_latent"] = global_latent.numpy()
     # model outputs of each pass, flattened to (SB*B'*K, 4) in ray-major order
     arrays["raw_coarse"] = torch.cat([r.reshape(-1, 4) for r in captured["raw"][:1]]).numpy()
     if "fine" in out:
@@ -495,6 +522,42 @@ def main():
         save(*gen_rays_case("gen_rays"))
     if want("frame32"):
         save(*frame_case("frame32"))
+    # --- confs the fused kernel does not implement (the callback path) ----
+    if want("alt_softplus"):
+        sc = synth.scene_srn(seed=0, n_rays=32, pick="hash")
+        save(*render_case("alt_softplus", d_hidden=512, d_latent=512, seed=31, scene=sc, n_coarse=64,
+                          n_fine=32, n_fine_depth=16, white_bkgd=True, rng_seed=12, opts=dict(beta=100.0)))
+    if want("alt_dh256"):
+        sc = synth.scene_srn(seed=0, n_rays=32, pick="hash")
+        save(*render_case("alt_dh256", d_hidden=256, d_latent=512, seed=32, scene=sc, n_coarse=64,
+                          n_fine=64, n_fine_depth=0, white_bkgd=True, rng_seed=13))
+    if want("alt_nl3"):
+        sc = synth.scene_nmr(seed=3, n_rays=32, channels=256)
+        save(*render_case("alt_nl3", d_hidden=512, d_latent=256, seed=33, scene=sc, n_coarse=64,
+                          n_fine=64, n_fine_depth=0, white_bkgd=True, rng_seed=14))
+    if want("alt_codevd"):
+        sc = synth.scene_srn(seed=0, n_rays=32, pick="hash")
+        save(*render_case("alt_codevd", d_hidden=512, d_latent=512, seed=34, scene=sc, n_coarse=64,
+                          n_fine=32, n_fine_depth=16, white_bkgd=True, rng_seed=15,
+                          opts=dict(use_code_viewdirs=True)))
+    if want("alt_spade_max"):
+        sc = synth.scene_multiview(seed=6, n_views=2, n_rays=32, channels=64, h_l=12, w_l=16)
+        save(*render_case("alt_spade_max", d_hidden=128, d_latent=64, seed=35, scene=sc, n_coarse=32,
+                          n_fine=16, n_fine_depth=0, white_bkgd=False, rng_seed=16,
+                          multi_obj_poses=sc["poses"][None], focal_override=sc["focal"][None],
+                          c_override=sc["c"][None], opts=dict(use_spade=True, combine_type="max")))
+    if want("alt_global"):
+        sc = synth.scene_srn(seed=0, n_rays=32, pick="hash", channels=64, h_l=16, w_l=16)
+        gl = torch.from_numpy(synth.hash_normal(77, (1, 128)))
+        save(*render_case("alt_global", d_hidden=256, d_latent=64, seed=36, scene=sc, n_coarse=32,
+                          n_fine=32, n_fine_depth=0, white_bkgd=True, rng_seed=17,
+                          opts=dict(global_latent_size=128), global_latent=gl))
+    if want("alt_zeros_pad"):
+        # grid_sample zeros padding: the target view sees past the source image's border
+        sc = synth.scene_srn(seed=0, n_rays=32, pick="hash", theta_tgt=75.0, channels=64, h_l=16, w_l=16)
+        save(*render_case("alt_zeros_pad", d_hidden=128, d_latent=64, seed=37, scene=sc, n_coarse=32,
+                          n_fine=32, n_fine_depth=8, white_bkgd=True, rng_seed=18,
+                          opts=dict(index_padding="zeros")))
     if want("fw_pointquery"):
         sc = synth.scene_srn(seed=0, n_rays=1)
         save(*point_query_case("fw_pointquery", seed=1, scene=sc, n_points=512))

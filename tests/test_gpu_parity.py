@@ -269,6 +269,40 @@ def test_point_query_dynamic_range(precision, lat_scale, w_scale, latent_proj):
                  atol=ATOL * max(1.0, mag))
 
 
+@pytest.mark.parametrize("latent_proj", [True, False])
+@pytest.mark.parametrize("precision", ["f16x3", "fp32"])
+def test_point_query_nan_point_stays_confined(precision, latent_proj):
+    """the f16x3 column maxima use NaN-propagating v_maximum3, so a NaN activation
+    makes its column's maximum NaN and that column is split unscaled.  A column of the LDS image is
+    ONE point (rows are channels), and a NaN channel reaches every channel of its point at the next
+    GEMM, as in torch, so the point is NaN either way; no other point of its tile is affected.
+    Checked: NaN view directions on 3 points of 3 different tiles; those points are NaN in the HIP
+    output and in the oracle, every other point matches the oracle within the tolerance."""
+    sd = synth.pixelnerf_state(5)
+    lat = synth.latent(11, 1, 512, 16, 16)
+    poses = synth.srn_poses([10.0])
+    focal = torch.tensor(40.0)
+    xyz = torch.from_numpy(synth.hash_sym(91, (1, 300, 3), 0.5))
+    vd = torch.nn.functional.normalize(torch.from_numpy(synth.hash_sym(92, (1, 300, 3), 1.0)), dim=-1)
+    bad = [5, 70, 200]
+    vd[0, bad] = float("nan")
+    scene = ref_cpu.Scene(lat, poses, focal, 64, 64, None)
+    with torch.no_grad():
+        ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, True, vd)
+    net = PixelNeRFNet(model_conf())
+    net.mlp_precision = precision
+    net.use_latent_proj = latent_proj
+    net.load_state_dict(sd, strict=False)
+    net = net.to(DEV).eval()
+    net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (64, 64))
+    with torch.no_grad():
+        out = net(xyz.to(DEV), coarse=True, viewdirs=vd.to(DEV)).cpu()
+    good = torch.ones(300, dtype=torch.bool)
+    good[bad] = False
+    assert bool(torch.isnan(ref[0, bad]).all()) and bool(torch.isnan(out[0, bad]).all())
+    assert_close(out[0, good], ref[0, good], "points beside NaN points")
+
+
 def heavy_tailed_state(seed):
     """Trained-like weight statistics for the accuracy check of the split arithmetics: every
     ResnetFC matrix gets log-normal row and column scales (exp(1.5 N), a ~e^+-4.5 spread per
@@ -609,14 +643,25 @@ def test_full_frame_dtu_ns3_properties_and_fixture_rows():
     print("cfg4 full frame: proven fine-bin flips on the fixture rows: %d" % n)
 
 
-def test_unsupported_config_fails_loudly():
+def test_unsupported_config_takes_callback_path_and_misuse_fails_loudly():
+    """A conf the fused kernel does not implement (here d_hidden = 256 for the coarse MLP)
+    renders through the callback path (tests/test_gpu_fallback.py pins it to the reference);
+    the fused path still refuses a model that was never encoded and CPU rays."""
     conf = model_conf()
     conf["mlp_coarse"] = dict(conf["mlp_coarse"], d_hidden=256)
     net = PixelNeRFNet(conf).to(DEV).eval()
+    assert "512" in net.fused_conf_reason()
     net.encode_latent(torch.zeros(1, 512, 8, 8, device=DEV), synth.srn_poses([0.0]).to(DEV),
                       torch.tensor(100.0, device=DEV), (64, 64))
-    with torch.no_grad(), pytest.raises(NotImplementedError):
-        net(torch.zeros(1, 4, 3, device=DEV), coarse=True, viewdirs=torch.zeros(1, 4, 3, device=DEV))
+    with torch.no_grad():
+        out = net(torch.zeros(1, 4, 3, device=DEV), coarse=True, viewdirs=torch.zeros(1, 4, 3, device=DEV))
+    assert out.shape == (1, 4, 4) and bool(torch.isfinite(out).all())
+    fused = PixelNeRFNet(model_conf()).to(DEV).eval()
+    assert fused.fused_conf_reason() is None
+    with torch.no_grad(), pytest.raises(NotImplementedError, match="encode"):
+        fused(torch.zeros(1, 4, 3, device=DEV), coarse=True, viewdirs=torch.zeros(1, 4, 3, device=DEV))
+    with torch.no_grad(), pytest.raises(ValueError, match="HIP device"):
+        NeRFRenderer(n_coarse=8)(net, torch.zeros(1, 4, 8))
 
 
 # ------------------------------------------------------------- video frame --
@@ -888,6 +933,19 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
     a = outs[2]
     w = a.coarse.weights
     assert bool((w >= 0).all()) and float(w.sum(-1).max()) <= 1.0 + 1e-5
+    # a normal render does not ask for z, and then mode 3's fine tiles read their
+    # depths from LDS only (no z_fine in HBM); that path too is bit-identical to mode 0
+    r.return_z = False
+    for mode in (3, 2):
+        r.march_mode = mode
+        with torch.no_grad():
+            torch.manual_seed(11)
+            o = r(net, rays, want_weights=True)
+        torch.cuda.synchronize()
+        for p in (("coarse", "fine") if kf > 0 else ("coarse",)):
+            assert "z" not in o[p]
+            for k in ("rgb", "depth", "weights"):
+                assert torch.equal(o[p][k], b[p][k]), ("return_z=False", mode, p, k)
 
 
 def test_march_modes_in_two_host_threads():
@@ -947,3 +1005,110 @@ def test_march_modes_in_two_host_threads():
             for p in ("coarse", "fine"):
                 for k in ("rgb", "depth", "weights", "z"):
                     assert torch.equal(o[p][k], ref[p][k]), (mode, p, k)
+
+
+# ------------------------------------------------------------- bind_parallel --
+def test_bind_parallel_replicas_render_fixture():
+    """nn.DataParallel (bind_parallel(net, gpus=[...]), nerf.py:354-371; gen_video.py:110,
+    train.py:93) re-replicates the network on every forward with torch.nn.parallel.replicate.
+    Here two replicas on device 0 (the one-GPU box) are built AFTER the original has packed
+    its weights and projected its latent; each renders half of fw_cfg2's rays with the
+    fixture's streams for those rays.  Each replica must pack and project from its own
+    parameters (the replicas used to inherit the original's packs through their
+    __dict__ copy), and the assembled render must match the reference fixture."""
+    from torch.nn.parallel import replicate
+
+    from pnr.renderer import DotMap, _RenderWrapper
+
+    cfg, arr = fixtures.load("fw_cfg2")
+    net = hip_net(cfg, arr)
+    # the reference moves the renderer to the device before bind_parallel (gen_video.py:106-110)
+    r = NeRFRenderer(n_coarse=cfg["n_coarse"], n_fine=cfg["n_fine"], n_fine_depth=cfg["n_fine_depth"],
+                     depth_std=cfg["depth_std"], white_bkgd=bool(cfg["white_bkgd"]),
+                     lindisp=bool(cfg["lindisp"])).to(DEV)
+    r.return_z = True
+    st = [arr[k].float() for k in ("u_coarse", "u_fine", "u_fine_jit", "n_depth")]
+    r.streams = tuple(st)
+    with torch.no_grad():
+        ref = r(net, arr["rays"].to(DEV), want_weights=True)   # the original packs + projects
+    orig_pack = net.mlp_coarse.__dict__["_pnr_pack"][3]
+    wrapped = _RenderWrapper(net, r, simple_output=False)
+    reps = replicate(wrapped, [0, 0], detach=True)
+    B = arr["rays"].shape[1]
+    half = B // 2
+    parts = []
+    for i, rep in enumerate(reps):
+        lo, hi = i * half, (B if i == len(reps) - 1 else (i + 1) * half)
+        rep.renderer.streams = tuple(t[lo:hi] for t in st)
+        with torch.no_grad():
+            o = rep(arr["rays"][:, lo:hi].to(DEV), want_weights=True)
+        m = rep.net.mlp_coarse
+        own = m.__dict__["_pnr_pack"]
+        assert own[0]() is m and own[3] is not orig_pack, "replica %d reused the original's pack" % i
+        assert m.__dict__["_pnr_proj"][0]() is m
+        parts.append(o)
+    torch.cuda.synchronize()
+    out = DotMap({p: DotMap({k: torch.cat([o[p][k] for o in parts], 1) for k in parts[0][p]})
+                  for p in ("coarse", "fine")})
+    compare_render("fw_cfg2/replicas", out, cfg, arr)
+    for p in ("coarse", "fine"):
+        for k in ("rgb", "depth", "weights", "z"):
+            assert torch.equal(out[p][k], ref[p][k]), (p, k)
+
+
+def test_bind_parallel_dataparallel_forward():
+    """The nn.DataParallel module bind_parallel returns for two device ids (both 0 here):
+    every forward re-replicates, each replica renders its scatter chunk of the rays with
+    counter-mode draws; the result has the right shapes and the composite invariants, and the
+    original's packs are never handed to a replica."""
+    cfg, arr = fixtures.load("fw_cfg2")
+    net = hip_net(cfg, arr)
+    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True).to(DEV)
+    par = r.bind_parallel(net, [0, 0], simple_output=False)
+    rays = arr["rays"].to(DEV)
+    with torch.no_grad():
+        net.hip_mlp(True), net.hip_proj(True)
+        for _ in range(2):
+            out = par(rays, want_weights=True)
+    torch.cuda.synchronize()
+    B = rays.shape[1]
+    for p in ("coarse", "fine"):
+        assert out[p]["rgb"].shape == (1, B, 3) and out[p]["depth"].shape == (1, B)
+        w = out[p]["weights"]
+        assert bool((w >= 0).all()) and float(w.sum(-1).max()) <= 1.0 + 1e-5
+        assert bool(torch.isfinite(out[p]["rgb"]).all())
+
+
+def test_single_launch_uses_each_pack_pe_table():
+    """march mode 3 runs the coarse and the fine tiles in one launch; the fine
+    tiles must read the positional-encoding table from the FINE pack's header.  Here the two packs
+    carry different tables (the fine MLP packed with another freq_factor, as two separately built
+    models could); mode 3 must stay bit-identical to mode 0, whose separate launches each read
+    their own pack."""
+    from pnr import torchops
+    from pnr.models import PositionalEncoding
+
+    cfg, arr = fixtures.load("fw_cfg2")
+    net = hip_net(cfg, arr)
+    ops_ = torchops.load()
+    rays = arr["rays"].reshape(-1, 8).to(DEV).contiguous()
+    B = rays.shape[0]
+    desc, pc = net.hip_mlp(True)
+    code2 = PositionalEncoding(6, 3, 2.5, True).to(DEV)
+    _, pf = net.mlp_fine.packed(code2, net.mlp_precision)
+    zc, zf = net.hip_proj(True), net.hip_proj(False)
+    outs = {}
+    for mode in (0, 3):
+        with torch.no_grad():
+            outs[mode] = ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, pf, zc, zf, rays,
+                                          B, 64, 64, 0, 0.01, True, False, None, None, None, None, 1234, 0, True,
+                                          True, [], mode)
+    torch.cuda.synchronize()
+    for a, b in zip(outs[0], outs[3]):
+        assert torch.equal(a, b)
+    # and the tables really differ: the fine pass with the coarse table is another render
+    with torch.no_grad():
+        other = ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, net.hip_mlp(False)[1], zc,
+                                 zf, rays, B, 64, 64, 0, 0.01, True, False, None, None, None, None, 1234, 0, True,
+                                 True, [], 0)
+    assert not torch.equal(other[3], outs[0][3])

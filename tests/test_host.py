@@ -254,3 +254,33 @@ def test_render_cfg_march_mode_is_per_call():
         assert lib.pnr_render_set_fused(2) == 2
     finally:
         lib.pnr_render_set_fused(prev)
+
+
+def test_callback_confs_and_state_dict_layout():
+    """Confs the fused kernel does not implement are recognised (fused_conf_reason), keep the
+    reference's state-dict layout (scale_z with use_spade, global_encoder.* with the global
+    encoder), and the callback forward refuses CPU tensors like the fused path."""
+    base = _conf_dict()
+    cases = {
+        "softplus": dict(base, mlp_coarse=dict(base["mlp_coarse"], beta=100.0)),
+        "d_hidden": dict(base, mlp_fine=dict(base["mlp_fine"], d_hidden=256)),
+        "latent": dict(base, encoder=dict(base["encoder"], num_layers=3)),
+        "viewdirs": dict(base, use_code_viewdirs=True),
+        "spade": dict(base, mlp_coarse=dict(base["mlp_coarse"], use_spade=True)),
+        "combine": dict(base, mlp_coarse=dict(base["mlp_coarse"], combine_type="max")),
+        "global": dict(base, use_global_encoder=True,
+                       global_encoder=dict(backbone="resnet34", pretrained=False, latent_size=128)),
+        "padding": dict(base, encoder=dict(base["encoder"], index_padding="zeros")),
+    }
+    for name, c in cases.items():
+        net = PixelNeRFNet(c)
+        assert net.fused_conf_reason() is not None, name
+        with pytest.raises(ValueError, match="HIP device"):
+            net(torch.zeros(1, 2, 3), coarse=True, viewdirs=torch.zeros(1, 2, 3))
+    assert PixelNeRFNet(base).fused_conf_reason() is None
+    sd = PixelNeRFNet(cases["spade"]).state_dict()
+    assert sd["mlp_coarse.scale_z.2.weight"].shape == (512, 512) and "mlp_fine.scale_z.0.weight" not in sd
+    g = PixelNeRFNet(cases["global"])
+    assert g.d_latent == 640 and g.mlp_coarse.lin_z[0].weight.shape == (512, 640)
+    assert g.state_dict()["global_encoder.fc.weight"].shape == (128, 512)
+    assert PixelNeRFNet(cases["viewdirs"]).d_in == 78

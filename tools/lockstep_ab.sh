@@ -1,7 +1,8 @@
 #!/bin/bash
 # Per-XCD lockstep pacing A/B: FETCH_SIZE (HBM/MALL bytes) and clock of the
 # cfg3 fine-pass launches per variant, then the alternating render A/B of tools/bench_ab.sh.
-# Build first (CPU): scripts/build_variant.sh lock1 WORKTREE -DPNR_LOCKSTEP=1 (and lock4: =4)
+# Build first (CPU): PATCH=tools/patches/lockstep.diff scripts/build_variant.sh lock1 WORKTREE -DPNR_LOCKSTEP=1
+# (and lock4: =4)
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 REPO=$(pwd)
 export TMPDIR=/tmp
