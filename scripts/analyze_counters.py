@@ -13,6 +13,7 @@ prints the mean over launches of:
   l2_hit         TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)
   l2_req_gb      (TCC_HIT_sum + TCC_MISS_sum) x 128 B: L2 requests of the launch (CU reads
                  of 16 B/lane coalesced rows arrive as 128-B line requests)
+  valu_active    SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (CUs * 4 SIMDs * clock cycles)
   hbm_gb         FETCH_SIZE x 2 (KB; gfx950 correction of MI355X_MICROARCH.md), when collected
 """
 import csv
@@ -80,6 +81,9 @@ def main():
             line.append("hbm_gb %.2f" % (m["FETCH_SIZE"] * 2 * 1024e-9))
         if "SQ_INSTS_VALU" in m and "SQ_INSTS_MFMA" in m:
             line.append("valu/mfma %.2f" % (m["SQ_INSTS_VALU"] / m["SQ_INSTS_MFMA"]))
+        if "SQ_ACTIVE_INST_VALU" in m and "GRBM_GUI_ACTIVE" in m:
+            # quad-cycles (MI355X_MICROARCH.md) of VALU issue, all waves, per SIMD cycle
+            line.append("valu_active %.3f" % (m["SQ_ACTIVE_INST_VALU"] * 4 / (CUS * 4 * clk * m["dur"])))
         print("  ".join(line))
 
 

@@ -1,5 +1,9 @@
-"""Times the encoder trunk's training work alone (forward + backward of conv1 .. layer3 + the
-channels-last latent, 4 x 3 x 128 x 128 SRN images) in NCHW and in channels_last memory format.
+"""Times the encoder trunk alone (conv1 .. layer3 + the channels-last latent, 4 x 3 x 128 x 128
+SRN images) in three forms, for the training step (train-mode BN, forward + backward + Adam) and
+for the render encode (eval mode, no grad):
+    nchw           the shipped form (MIOpen convolutions, NCHW activations)
+    channels_last  module and input in torch.channels_last (MIOpen's NHWC kernels)
+    native         MIOpen disabled (torch.backends.cudnn.enabled = False: ATen's im2col + GEMM)
     python tools/encoder_probe.py"""
 import os
 import sys
@@ -11,7 +15,23 @@ from pnr.encoder import SpatialEncoder  # noqa: E402
 
 torch.backends.cudnn.benchmark = True
 dev = torch.device("cuda:0")
-for fmt in ("nchw", "channels_last", "nchw", "channels_last"):
+
+
+def timed(fn, n=20):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n
+
+
+for fmt in ("nchw", "channels_last", "native", "nchw", "channels_last", "native"):
+    torch.backends.cudnn.enabled = fmt != "native"
     torch.manual_seed(0)
     enc = SpatialEncoder(pretrained=False).to(dev)
     x = torch.randn(4, 3, 128, 128, device=dev)
@@ -22,17 +42,14 @@ for fmt in ("nchw", "channels_last", "nchw", "channels_last"):
 
     def step():
         opt.zero_grad(set_to_none=True)
-        lat = enc(x)
+        enc(x)
         (enc.latent_cl * 1e-3).sum().backward()
         opt.step()
 
-    for _ in range(5):
-        step()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(20):
-        step()
-    e1.record()
-    torch.cuda.synchronize()
-    print("%-14s %.3f ms per step" % (fmt, e0.elapsed_time(e1) / 20))
+    enc.train()
+    t_train = timed(step)
+    enc.eval()
+    with torch.no_grad():
+        t_enc = timed(lambda: enc(x))
+    print("%-14s train step %.3f ms   eval encode %.3f ms" % (fmt, t_train, t_enc), flush=True)
+torch.backends.cudnn.enabled = True
