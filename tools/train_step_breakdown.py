@@ -40,6 +40,49 @@ def main():
     for g in gaps[:12]:
         print("  %7.3f ms  after %s  before %s" % (g[0] / 1e6, g[1], g[2]))
 
+    phases(rows)
+
+
+def phases(rows):
+    """Wall span and kernel-busy time of the step's regions, delimited by landmark kernels: the
+    step is the dispatches after the last-but-one Adam (FusedOptimizer) kernel group up to the last
+    one; regions end at the first coarse / fine forward MLP, the first / second k_mlp_bwd, the
+    last k_points_in_bwd and the first Adam kernel."""
+    opt = [i for i, r in enumerate(rows) if "FusedOptimizer" in r["Kernel_Name"]]
+    if len(opt) < 2:
+        return
+    # last Adam group: consecutive optimizer dispatches at the end
+    last = opt[-1]
+    first_of_last = last
+    while first_of_last - 1 in opt:
+        first_of_last -= 1
+    prev = max(i for i in opt if i < first_of_last)
+    seg = rows[prev + 1: last + 1]
+    names = [r["Kernel_Name"] for r in seg]
+    fwd = [i for i, n in enumerate(names) if "k_point_mlp" in n]
+    bwd = [i for i, n in enumerate(names) if "k_mlp_bwd" in n]
+    pin = [i for i, n in enumerate(names) if "k_points_in_bwd" in n]
+    adam = [i for i, n in enumerate(names) if "FusedOptimizer" in n]
+    if len(fwd) < 2 or len(bwd) < 2 or not pin or not adam:
+        return
+    cuts = [("encode (+ coarse draws)", fwd[0]), ("coarse forward MLP", fwd[0] + 1),
+            ("fine draws", fwd[1]), ("fine forward MLP", fwd[1] + 1),
+            ("loss + composite backward", bwd[0]), ("first MLP backward (+ wgrad, input bwd)", bwd[1]),
+            ("second MLP backward (+ wgrad, input bwd)", pin[-1] + 1),
+            ("encoder backward + grad glue", adam[0]), ("Adam", len(seg))]
+    print("step regions (wall span incl. idle / kernel busy):")
+    lo = 0
+    t_prev_end = int(seg[0]["Start_Timestamp"])
+    for name, hi in cuts:
+        part = seg[lo:hi]
+        if part:
+            t0 = t_prev_end
+            t1 = max(int(r["End_Timestamp"]) for r in part)
+            busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in part)
+            print("  %-44s %7.3f ms  busy %7.3f ms  %4d dispatches" % (name, (t1 - t0) / 1e6, busy / 1e6, len(part)))
+            t_prev_end = t1
+        lo = hi
+
 
 if __name__ == "__main__":
     main()
