@@ -248,6 +248,9 @@ def make_net(dev, precision, latent_proj, use_first_pool=True):
 
 def cfg3_leg(args, dev, rank, world, probe):
     net = make_net(dev, args.precision, not args.no_latent_proj, use_first_pool=False)
+    # the eval encode runs the BN-folded trunk replayed as one HIP graph (pnr.encoder.InferenceTrunk);
+    # --encoder-eager: the module's own conv / BN / relu launches (A/B)
+    net.encoder.infer_fast = not getattr(args, "encoder_eager", False)
     img, src, focal, rays = nmr_inputs(dev)
     n_all = rays.shape[0]
     start, end = pdist.shard_range(n_all, rank, world)
@@ -665,13 +668,17 @@ def cpu_baselines(sd, nmr, net3, dev, n_rays):
     oracle scene of the sample)."""
     from oracle import ref_cpu
 
-    def median_run(fn):
+    def median_run(fn, give_up=None):
+        """Median of 3 timed runs after a warm-up; one run only when it already takes longer
+        than ``give_up`` seconds (a thread count far slower than one already measured)."""
         fn(warm=True)
         times, out = [], None
         for _ in range(3):
             t0 = time.perf_counter()
             out = fn(warm=False)
             times.append(time.perf_counter() - t0)
+            if give_up is not None and times[-1] > give_up:
+                break
         return statistics.median(times), times, out
 
     def runner(scene, rays, streams, kc, kf):
@@ -691,14 +698,16 @@ def cpu_baselines(sd, nmr, net3, dev, n_rays):
     # be held to fewer CPUs (affinity / the job's CPU share, OMP_NUM_THREADS) than the host
     # has, so the headline sample is timed at both counts; `value` is the faster, and both
     # are reported
-    counts = [os.cpu_count() or 1]
     share = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "0")) or 1 << 30)
-    if share not in counts:
-        counts.append(share)
+    counts = [share]
+    if (os.cpu_count() or 1) != share:
+        counts.append(os.cpu_count() or 1)
     by_threads = {}
     for n in counts:
         torch.set_num_threads(n)
-        t, runs, out = median_run(runner(scene3, rays3[idx].cpu(), st3, KC, KF))
+        fastest = min((v[0] for v in by_threads.values()), default=None)
+        t, runs, out = median_run(runner(scene3, rays3[idx].cpu(), st3, KC, KF),
+                                  give_up=None if fastest is None else 3 * fastest)
         by_threads[n] = (t, runs, out)
     best = min(by_threads, key=lambda n: by_threads[n][0])
     torch.set_num_threads(best)
@@ -717,7 +726,8 @@ def cpu_baselines(sd, nmr, net3, dev, n_rays):
                             for n, v in by_threads.items()},
                 sample="%d rays spread evenly over the cfg3 98,304-ray batch x (64+64) samples, "
                        "oracle/ref_cpu.py, median of 3 runs (%s s) at %d threads (the faster of "
-                       "os.cpu_count() and the process's CPU share, by_threads)"
+                       "os.cpu_count() and the process's CPU share, by_threads; a count 3x slower than "
+                       "the faster after one run is not repeated)"
                        % (n_rays, fmt(runs3), best),
                 cfg1_full=dict(value=round(256 / t1, 2), unit="rays/s",
                                sample="cfg1 at full size: 256 rays x 32 coarse, median of 3 (%s s)" % fmt(runs1)),
@@ -842,6 +852,8 @@ def main():
     ap.add_argument("--no-compare", action="store_true", help="skip the f32-MFMA comparison frame")
     ap.add_argument("--train-steps", type=int, default=5)
     ap.add_argument("--precision", default="f16x3", choices=sorted(PEAK_BY_PRECISION))
+    ap.add_argument("--encoder-eager", action="store_true",
+                    help="cfg3 encode by the module's conv / BN / relu launches instead of the folded trunk's graph")
     ap.add_argument("--no-latent-proj", action="store_true",
                     help="per-point lin_z GEMMs on the gathered latent (A/B against the projection)")
     ap.add_argument("--unfused", action="store_true",

@@ -12,6 +12,7 @@ The hot path consumes the latent channels-LAST; ``latent_cl`` keeps that copy.
 """
 import ctypes
 import warnings
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -65,6 +66,122 @@ class LatentChannelsLast(torch.autograd.Function):
                 grads.append(torch.ops.aten.upsample_bilinear2d_backward(
                     gi, [h, w], list(shp), True, None, None))
         return tuple(grads)
+
+
+class InferenceTrunk:
+    """The encoder trunk for rendering (eval mode, no autograd; encoder.py:135-164's forward with
+    the BatchNorms on their running statistics, what gen_video.py / eval.py run after .eval()):
+
+    * every BatchNorm is folded into the convolution before it, W' = W s and b' = beta - mu s with
+      s = gamma / sqrt(var + eps) per output channel (the same affine map, one rounding apart);
+    * ReLUs and residual adds run in place;
+    * the trunk and the channels-last latent kernel (``pnr_latent_channels_last``) are captured
+      once per input shape as one HIP graph and replayed: the eval encode is ~140 small launches
+      whose host-side issue, not their GPU time, sets its duration (the fixed per-rank cost at
+      N = 8).
+
+    The folded weights are recomputed in place (the graph reads the same buffers) whenever a
+    convolution weight, BatchNorm parameter or running statistic changed (tensor versions and
+    storage), so optimizer steps and load_state_dict are seen."""
+
+    def __init__(self, enc, device):
+        self.owner = weakref.ref(enc)
+        self.device = device
+        m = enc.model
+        self.layers = [m.layer1, m.layer2, m.layer3, m.layer4][:max(enc.num_layers - 1, 0)]
+        pairs = [(m.conv1, m.bn1)]
+        for layer in self.layers:
+            for blk in layer:
+                pairs += [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2)]
+                if blk.downsample is not None:
+                    pairs.append((blk.downsample[0], blk.downsample[1]))
+        self.pairs = pairs
+        self.folded = {id(c): (torch.empty_like(c.weight), torch.empty(c.out_channels, device=device))
+                       for c, _ in pairs}
+        self.tensors = list(self._tensors())
+        self.key = None
+        self.graphs = {}          # (shape, dtype, strides) -> (graph, static input, static latent)
+        self.use_graph = True
+
+    def _tensors(self):
+        for c, b in self.pairs:
+            yield c.weight
+            for t in (b.weight, b.bias, b.running_mean, b.running_var):
+                if t is not None:
+                    yield t
+
+    def refresh(self):
+        # versions of every folded-in tensor (in-place updates) and the conv weights' storage
+        # (replaced data); ~30 us per encode
+        key = (tuple(t._version for t in self.tensors), tuple(c.weight.data_ptr() for c, _ in self.pairs))
+        if key == self.key:
+            return
+        with torch.no_grad():
+            for c, b in self.pairs:
+                w, bias = self.folded[id(c)]
+                s = torch.rsqrt(b.running_var + b.eps)
+                if b.weight is not None:
+                    s = s * b.weight
+                w.copy_(c.weight * s.view(-1, 1, 1, 1))
+                bias.copy_(-b.running_mean * s if b.bias is None else b.bias - b.running_mean * s)
+        self.key = key
+
+    def trunk(self, x):
+        enc = self.owner()
+        m = enc.model
+        f = self.folded
+
+        def conv(c, x, relu=True):
+            w, b = f[id(c)]
+            y = F.conv2d(x, w, b, c.stride, c.padding, c.dilation, c.groups)
+            return torch.relu_(y) if relu else y
+
+        x = conv(m.conv1, x)
+        maps = [x]
+        if self.layers and enc.use_first_pool:
+            x = m.maxpool(x)
+        for layer in self.layers:
+            for blk in layer:
+                idt = x if blk.downsample is None else conv(blk.downsample[0], x, relu=False)
+                y = conv(blk.conv2, conv(blk.conv1, x), relu=False)
+                x = torch.relu_(y.add_(idt))
+            maps.append(x)
+        return _latent_channels_last(maps)
+
+    def _capture(self, x, key):
+        xin = x.clone()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):   # MIOpen solver search and allocator warm-up, outside the capture
+            for _ in range(2):
+                self.trunk(xin)
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        try:
+            # thread_local: other threads' HIP calls (the RCCL process group's watchdog at N > 1)
+            # do not invalidate this thread's capture
+            with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                out = self.trunk(xin)
+        except RuntimeError as e:   # a library call that cannot be captured: eager launches from now on
+            warnings.warn("pnr: encoder trunk graph capture failed (%s); eager launches" % e)
+            self.use_graph = False
+            return None
+        self.graphs[key] = (graph, xin, out)
+        return self.graphs[key]
+
+    def run(self, x):
+        """(NS, H_l, W_l, C) channels-last latent of images x (NS, 3, H, W)."""
+        self.refresh()
+        key = (tuple(x.shape), x.dtype, x.stride())
+        g = self.graphs.get(key)
+        if g is None and self.use_graph:
+            g = self._capture(x, key)
+        if g is None:
+            return self.trunk(x)
+        graph, xin, out = g
+        xin.copy_(x)
+        graph.replay()
+        return out.clone()   # the graph's output buffer is rewritten by the next replay
 
 
 class BasicBlock(nn.Module):
@@ -160,6 +277,9 @@ class SpatialEncoder(nn.Module):
         # channels-last copy (NS, H_l, W_l, C) read by the HIP gather; a buffer so that
         # nn.DataParallel replicas get their own device copy
         self.register_buffer("latent_cl", torch.empty(0), persistent=False)
+        # eval-mode encodes on the device run the folded, graph-replayed trunk (InferenceTrunk)
+        self.infer_fast = True
+        self._infer = None
 
     def set_latent(self, latent):
         """Install a feature map (NS, C, H_l, W_l) as forward() would (encoder.py:160-163)."""
@@ -176,6 +296,8 @@ class SpatialEncoder(nn.Module):
                               align_corners=True if self.feature_scale > 1.0 else None,
                               recompute_scale_factor=True)
         x = x.to(device=self.latent.device)
+        if self._use_infer(x):
+            return self.set_latent_cl(self._infer.run(x))
         m = self.model
         x = m.relu(m.bn1(m.conv1(x)))
         latents = [x]
@@ -201,19 +323,34 @@ class SpatialEncoder(nn.Module):
                                        align_corners=True)
         return self.set_latent(torch.cat(latents, dim=1))
 
-    def set_latent_maps(self, maps):
-        """encoder.py:150-163 on the HIP device without the NCHW concat + transpose:
-        ``pnr_latent_channels_last`` upsamples (bilinear, align_corners) and concatenates
-        the trunk maps straight into the channels-last latent the ray march reads;
-        ``latent`` is its NCHW view (no copy).  Under autograd the gradient flows back
-        through each map's upsample adjoint (``LatentChannelsLast``)."""
-        out = LatentChannelsLast.apply(*maps)
+    def _use_infer(self, x):
+        """The eval-mode inference trunk (InferenceTrunk) applies: no autograd, module in eval
+        mode (BatchNorm on its running statistics), BatchNorm layers, a HIP device, the
+        bilinear channels-last latent."""
+        if not (self.infer_fast and x.is_cuda and not self.training and not torch.is_grad_enabled()
+                and self.upsample_interp == "bilinear" and isinstance(self.model.bn1, nn.BatchNorm2d)
+                and self.model.bn1.track_running_stats):
+            return False
+        if self._infer is None or self._infer.device != x.device or self._infer.owner() is not self:
+            self._infer = InferenceTrunk(self, x.device)
+        return True
+
+    def set_latent_cl(self, out):
+        """Install a channels-last latent (NS, H_l, W_l, C) with its NCHW view."""
         h, w = out.shape[1], out.shape[2]
         self.latent = out.permute(0, 3, 1, 2)
         ls = device_const((w, h), out.device)
         self.latent_scaling = ls / (ls - 1) * 2.0
         self.latent_cl = out
         return self.latent
+
+    def set_latent_maps(self, maps):
+        """encoder.py:150-163 on the HIP device without the NCHW concat + transpose:
+        ``pnr_latent_channels_last`` upsamples (bilinear, align_corners) and concatenates
+        the trunk maps straight into the channels-last latent the ray march reads;
+        ``latent`` is its NCHW view (no copy).  Under autograd the gradient flows back
+        through each map's upsample adjoint (``LatentChannelsLast``)."""
+        return self.set_latent_cl(LatentChannelsLast.apply(*maps))
 
     def index(self, uv, cam_z=None, image_size=(), z_bounds=None):
         """Bilinear feature lookup at image points (encoder.py:80-109); utility only —

@@ -770,6 +770,54 @@ def test_latent_channels_last_matches_torch_upsample_concat():
     torch.testing.assert_close(cl_hip, enc.latent_cl.detach(), atol=1e-4, rtol=1e-5)
 
 
+def test_eval_encode_inference_trunk_matches_module_path():
+    """The eval-mode encode (pnr.encoder.InferenceTrunk: BatchNorm folded into the convolutions,
+    trunk + latent kernel replayed as one HIP graph) against the module's own conv / BN / relu
+    forward on the same weights, with non-trivial running statistics; a second image replays the
+    same graph; an in-place parameter change is picked up; returned latents are not aliased."""
+    from pnr.encoder import SpatialEncoder
+
+    g = torch.Generator().manual_seed(3)
+    enc = SpatialEncoder(pretrained=False)
+    for mod in enc.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            c = mod.num_features
+            mod.running_mean.copy_(torch.randn(c, generator=g) * 0.2)
+            mod.running_var.copy_(torch.rand(c, generator=g) * 1.5 + 0.25)
+            mod.weight.data.copy_(torch.rand(c, generator=g) + 0.5)
+            mod.bias.data.copy_(torch.randn(c, generator=g) * 0.1)
+    enc = enc.to(DEV).eval()
+    imgs = [(torch.rand(2, 3, 64, 80, generator=g) * 2 - 1).to(DEV) for _ in range(2)]
+
+    def encode(img, fast):
+        enc.infer_fast = fast
+        with torch.no_grad():
+            enc(img)
+        return enc.latent_cl.clone(), enc.latent_cl
+
+    def check(got, want):
+        scale = want.abs().max().item()
+        d = (got - want).abs().max().item()
+        assert d <= 2e-5 * scale, (d, scale)   # fp32 conv spread, relative to the latent's range
+
+    refs = [encode(x, False)[0] for x in imgs]
+    first, first_buf = encode(imgs[0], True)
+    assert enc._infer is not None and enc._infer.use_graph and len(enc._infer.graphs) == 1
+    second, _ = encode(imgs[1], True)            # same shape: the captured graph, new input
+    assert len(enc._infer.graphs) == 1
+    check(first, refs[0])
+    check(second, refs[1])
+    assert torch.equal(first_buf, first)         # the first call's latent survived the replay
+    again, _ = encode(imgs[0], True)             # a replay of the same input (MIOpen's convolution
+    check(again, refs[0])                        # solvers are not all bitwise repeatable)
+    with torch.no_grad():
+        enc.model.layer2[1].bn2.bias.add_(0.3)   # an in-place update: the fold is refreshed
+    ref3 = encode(imgs[0], False)[0]
+    got3, _ = encode(imgs[0], True)
+    assert not torch.equal(got3, first)
+    check(got3, ref3)
+
+
 # ----------------------------------------------------- coarse-output reuse --
 @pytest.mark.parametrize("kfd", [0, 16])
 def test_fine_pass_reuses_coarse_outputs_when_mlp_fine_is_none(kfd):

@@ -284,3 +284,42 @@ def test_callback_confs_and_state_dict_layout():
     assert g.d_latent == 640 and g.mlp_coarse.lin_z[0].weight.shape == (512, 640)
     assert g.state_dict()["global_encoder.fc.weight"].shape == (128, 512)
     assert PixelNeRFNet(cases["viewdirs"]).d_in == 78
+
+
+def test_inference_trunk_folds_batchnorm():
+    """pnr.encoder.InferenceTrunk (the eval-mode encode): every folded convolution equals the
+    module's conv + BatchNorm on its running statistics (CPU tensors; the graph replay and the
+    latent kernel are covered by test_gpu_parity), the fold follows in-place parameter updates,
+    and CPU tensors or train mode keep the module path."""
+    import torch.nn.functional as F
+    from pnr.encoder import InferenceTrunk, SpatialEncoder
+
+    g = torch.Generator().manual_seed(0)
+    enc = SpatialEncoder(pretrained=False)
+    for mod in enc.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            c = mod.num_features
+            mod.running_mean.copy_(torch.randn(c, generator=g))
+            mod.running_var.copy_(torch.rand(c, generator=g) + 0.1)
+            mod.weight.data.copy_(torch.randn(c, generator=g))
+            mod.bias.data.copy_(torch.randn(c, generator=g))
+    enc.eval()
+    t = InferenceTrunk(enc, torch.device("cpu"))
+    t.refresh()
+    assert len(t.pairs) == 1 + 2 * (3 + 4 + 6) + 2   # conv1, layer1-3 blocks, 2 downsamples
+    with torch.no_grad():
+        for conv, bn in t.pairs:
+            x = torch.randn(1, conv.in_channels, 12, 12, generator=g)
+            w, b = t.folded[id(conv)]
+            got = F.conv2d(x, w, b, conv.stride, conv.padding)
+            want = bn(conv(x))
+            assert (got - want).abs().max() <= 1e-4 * want.abs().max(), conv
+        enc.model.layer3[0].bn1.bias.add_(1.0)
+    t.refresh()
+    conv, bn = next(p for p in t.pairs if p[1] is enc.model.layer3[0].bn1)
+    x = torch.randn(1, conv.in_channels, 8, 8, generator=g)
+    with torch.no_grad():
+        got = F.conv2d(x, *t.folded[id(conv)], conv.stride, conv.padding)
+        assert (got - bn(conv(x))).abs().max() <= 1e-4 * got.abs().max()
+    with torch.no_grad():
+        assert not enc._use_infer(torch.zeros(1, 3, 8, 8))      # CPU input: module path

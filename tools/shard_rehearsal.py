@@ -29,6 +29,7 @@ def main():
 
     class A:
         precision, no_latent_proj, steps, warmup = "f16x3", False, 10, 2
+        encoder_eager = os.environ.get("ENCODER_EAGER") == "1"   # A/B of pnr.encoder.InferenceTrunk
 
     for n in worlds:
         bench.pdist.shard_range = lambda total, rank, world, n=n: orig(total, 0, n)
@@ -37,7 +38,7 @@ def main():
         ms = 1e3 * elapsed / A.steps
         kern = sum(v for k, v in avg.items() if k.startswith(("mlp_", "sample_", "composite_")))
         print(json.dumps({
-            "world": n, "rays_per_rank": e - s, "ms_per_step": round(ms, 3),
+            "world": n, "encoder": "eager" if A.encoder_eager else "folded trunk graph", "rays_per_rank": e - s, "ms_per_step": round(ms, 3),
             "projected_rays_per_s": round(n * (e - s) / (ms / 1e3), 1),
             "encode_ms": round(enc_ms, 3),
             "render_kernels_ms_per_chunk": {k: round(v, 4) for k, v in avg.items()},
