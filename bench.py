@@ -346,7 +346,8 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
     data: encode SB x NS source images (ResNet34 trunk), render SB x B' rays with the shipped
     conf (64 coarse + 32 fine incl. 16 depth, white background) through the HIP training path
     (pnr/train.py), MSE(coarse) + MSE(fine) (conf/default.conf:77-78), backward, bucketed
-    gradient mean over RCCL/xGMI (pnr.dist.allreduce_grads), Adam lr 1e-4 (trainer.py:49).
+    gradient mean over RCCL/xGMI overlapped with the backward (pnr.dist.GradReducer), Adam lr 1e-4
+    (trainer.py:49).
     Weak scaling: SB x B' rays per rank.  Returns the result dict (max-over-ranks timing)."""
     from pnr.models import make_model
 
@@ -379,13 +380,18 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
     target = torch.rand(sb, per, 3, device=dev, generator=g)
     mse = torch.nn.functional.mse_loss
 
+    # gradient mean overlapped with the backward: buckets go out from the grad hooks as they fill
+    # (the MLP buckets under the encoder's backward), the rest after backward()
+    reducer = pdist.GradReducer(params, world)
+
     def step():
         opt.zero_grad(set_to_none=True)
         net.encode(images, src_poses, focal)
         out = renderer(net, rays, want_weights=True)
         loss = mse(out.coarse.rgb, target) + mse(out.fine.rgb, target)
+        reducer.arm()
         loss.backward()
-        pdist.allreduce_grads(params, world)
+        reducer.finish()
         opt.step()
         return loss
 
@@ -465,7 +471,8 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
         "arithmetic": arith + " (pnr/train.py)",
         "config": {"workload": "cfg5: SB=%d objects x %d rays per rank, %d source view(s), 64 coarse + 32 fine "
                                "(16 depth)" % (sb, per, ns), "global_batch_rays": sb * per * world,
-                   "parallelism": "data parallel, 1 process per GPU, bucketed RCCL all-reduce (32 MB buckets)",
+                   "parallelism": "data parallel, 1 process per GPU, bucketed RCCL all-reduce (32 MB buckets) "
+                                  "launched from the backward's grad hooks",
                    "encoder_batchnorm": bn + (" (statistics all-reduced over the ranks, pnr.dist.SyncBatchNorm2d)"
                                               if bn == "sync" else ""),
                    "launch": "one HIP graph per step" if graph else "eager"},

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 
 __all__ = ["shard_range", "env_rank", "init_from_env", "max_over_ranks", "render_sharded",
-           "gather_to_rank0", "allreduce_grads", "SyncBatchNorm2d", "FrozenBatchNorm2d",
+           "gather_to_rank0", "allreduce_grads", "GradReducer", "SyncBatchNorm2d", "FrozenBatchNorm2d",
            "set_batchnorm_mode"]
 
 # xGMI is point-to-point (7 links x ~153 GB/s per GPU): RCCL's ring all-reduce is per-link
@@ -119,6 +119,96 @@ def allreduce_grads(params, world, bucket_bytes=BUCKET_BYTES):
             o += g.numel()
         n += 1
     return n
+
+
+class GradReducer:
+    """The data-parallel gradient mean of ``allreduce_grads``, overlapped with the backward (what
+    DDP's reducer does for the reference's DataParallel training).
+
+    A post-accumulate-grad hook on every parameter appends it to the open bucket as its gradient
+    lands. A bucket that reaches ``bucket_bytes`` is flattened and all-reduced (SUM) with
+    ``async_op=True``. RCCL runs it on its own stream while autograd goes on, so the MLP buckets,
+    which are ready first, reduce under the encoder's backward. ``finish()`` after ``backward()``
+    launches the last bucket, waits, scales by 1 / world and unpacks in place.
+
+    Autograd visits the graph in the same order on every rank, so every rank launches the same
+    buckets in the same order. A parameter whose gradient accumulates again after its bucket was
+    launched (a module used twice in one step) is reduced once more, whole, in ``finish()``.
+
+    Usage per step: ``r.arm(); loss.backward(); r.finish()``. World size 1: no hooks, no work."""
+
+    def __init__(self, params, world, bucket_bytes=BUCKET_BYTES):
+        self.world = world
+        self.bucket_bytes = bucket_bytes
+        self.armed = False
+        self._reset()
+        self.hooks = []
+        if world > 1:
+            self.hooks = [p.register_post_accumulate_grad_hook(self._ready) for p in params if p.requires_grad]
+
+    def _reset(self):
+        self.open, self.open_bytes = [], 0
+        self.flights = []      # (work, flat, params) of launched buckets
+        self.launched = set()  # id() of params in launched buckets
+        self.seen = set()      # id() of params in the open bucket
+        self.late = []         # params accumulated again after their bucket was launched
+
+    def _ready(self, p):
+        if not self.armed:
+            return
+        if id(p) in self.launched:
+            if all(q is not p for q in self.late):
+                self.late.append(p)
+            return
+        if id(p) in self.seen:
+            return   # accumulated again while its bucket is still open: the bucket reads .grad at launch
+        self.seen.add(id(p))
+        self.open.append(p)
+        self.open_bytes += p.grad.numel() * 4
+        if self.open_bytes >= self.bucket_bytes:
+            self._launch()
+
+    def _launch(self):
+        if not self.open:
+            return
+        ps, self.open, self.open_bytes = self.open, [], 0
+        self.seen.clear()
+        flat = torch.cat([p.grad.reshape(-1).float() for p in ps])
+        self.flights.append((dist.all_reduce(flat, op=dist.ReduceOp.SUM, async_op=True), flat, ps))
+        self.launched.update(id(p) for p in ps)
+
+    def arm(self):
+        """Before ``loss.backward()``."""
+        self._reset()
+        self.armed = self.world > 1
+
+    def finish(self):
+        """After ``loss.backward()``: the gradients are the mean over the ranks. Returns the
+        number of collectives issued."""
+        if not self.armed:
+            return 0
+        self._launch()
+        n = len(self.flights)
+        late = {id(p) for p in self.late}
+        for work, flat, ps in self.flights:
+            work.wait()
+            flat.mul_(1.0 / self.world)
+            o = 0
+            for p in ps:
+                k = p.grad.numel()
+                if id(p) not in late:
+                    p.grad.copy_(flat[o: o + k].view_as(p.grad))
+                o += k
+        if self.late:
+            n += allreduce_grads(self.late, self.world, self.bucket_bytes)
+        self.armed = False
+        self._reset()
+        return n
+
+    def remove(self):
+        for h in self.hooks:
+            h.remove()
+        self.hooks = []
 
 
 # ---- encoder BatchNorm across ranks (SURVEY §8(e) "semantics difference to resolve") ------

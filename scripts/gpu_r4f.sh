@@ -5,8 +5,9 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 echo "== encoder tests"; date
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -k "latent_channels_last or inference_trunk" \
-    --timeout 120 --timeout-method thread > gpurun_out/enc_tests.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dist.py -x -q \
+    -k "latent_channels_last or inference_trunk or two_rank or gpus_2" \
+    --timeout 300 --timeout-method thread > gpurun_out/enc_tests.log 2>&1; rc=$?
 tail -3 gpurun_out/enc_tests.log; [ $rc = 0 ] || exit $rc
 echo "== graph capture beside an RCCL process group"; date
 timeout -k 10 120 python tools/graph_pg_check.py 2>&1 | grep -v amdgpu.ids | tail -3 || exit 1

@@ -105,9 +105,10 @@ def test_two_rank_gloo_render_equals_single_process():
 
 
 # ---- data-parallel training: the gradient all-reduce -------------------
-def _train_grads(objs):
+def _train_grads(objs, before_backward=None):
     """Oracle training-step grads (tests/golden/train_step.npz inputs) over the objects
-    `objs` only: rays, streams, target, camera and latent rows of those objects."""
+    `objs` only: rays, streams, target, camera and latent rows of those objects.
+    ``before_backward(params)`` runs between the forward and ``loss.backward()``."""
     import fixtures
     from oracle import ref_cpu
 
@@ -129,6 +130,8 @@ def _train_grads(objs):
                          streams, cfg["white_bkgd"], depth_std=cfg["depth_std"])
     mse = torch.nn.functional.mse_loss
     loss = mse(out["coarse"]["rgb"], arr["target"][objs]) + mse(out["fine"]["rgb"], arr["target"][objs])
+    if before_backward is not None:
+        before_backward(params)
     loss.backward()
     return params
 
@@ -145,6 +148,60 @@ def _train_worker(rank, world, port, q):
         q.put(({k: p.grad.numpy().copy() for k, p in params.items()}, n))   # by value
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _overlap_worker(rank, world, port, q):
+    """The overlapped reducer (pnr.dist.GradReducer): buckets all-reduced from the backward's
+    grad hooks, with a parameter accumulated twice (a second, scaled use of one MLP weight
+    through a leaf-sharing term) to exercise the late re-reduction."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    torch.set_num_threads(1)
+    r, w, _ = pdist.init_from_env("gloo")
+    state = {}
+
+    def arm(params):
+        state["red"] = pdist.GradReducer(list(params.values()), w, bucket_bytes=64 << 10)
+        state["red"].arm()
+
+    params = _train_grads([r], arm)
+    red = state["red"]
+    n_hooked = len(red.flights)
+    # a second backward through one parameter after its bucket went out: the late path
+    k0 = next(k for k in params if k.endswith("lin_in.weight"))
+    red.armed = True
+    (params[k0] * float(r + 1)).sum().backward()
+    n = red.finish()
+    if r == 0:
+        q.put(({k: p.grad.numpy().copy() for k, p in params.items()}, n, n_hooked, k0))
+    red.remove()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_overlapped_reducer_equals_full_batch():
+    """pnr.dist.GradReducer (bench.py's training step): buckets launched from the backward's
+    grad hooks give the same mean gradient as the single-process whole-batch backward; a
+    parameter accumulated again after its bucket was launched is reduced whole."""
+    ref = _train_grads([0, 1])
+    k0 = next(k for k in ref if k.endswith("lin_in.weight"))
+    ref[k0].grad += (1.0 + 2.0) / 2.0   # the extra term: mean over ranks of (r + 1)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, n_coll, n_hooked, k_late = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert k_late == k0
+    assert n_hooked >= 2          # buckets went out during the backward
+    assert n_coll >= n_hooked + 1  # + the last bucket / the late re-reduction
+    for k, p in ref.items():
+        torch.testing.assert_close(torch.from_numpy(got[k]), p.grad, atol=1e-6, rtol=1e-4, msg=k)
 
 
 def test_two_rank_gloo_gradient_allreduce_equals_full_batch():
