@@ -27,7 +27,7 @@ def _imread_rgb(path):
     from PIL import Image
 
     with Image.open(path) as im:
-        a = np.asarray(im)
+        a = np.array(im)   # a writable copy
     if a.ndim == 2:                      # greyscale: imageio returns (H, W)
         a = np.repeat(a[..., None], 3, axis=-1)
     return a[..., :3]
@@ -71,60 +71,48 @@ class SRNDataset(torch.utils.data.Dataset):
     def __len__(self):
         return len(self.intrins)
 
+    @staticmethod
+    def _intrinsics(path):
+        """(focal, cx, cy) from line 1 of intrinsics.txt ("f cx cy _"; the last line's "H W" is
+        not used: the image itself fixes the size)."""
+        with open(path, "r") as f:
+            first = f.readline().split()
+        return float(first[0]), float(first[1]), float(first[2])
+
+    def _view(self, rgb_path, pose_path):
+        """One view: the balanced image tensor, its foreground mask (every channel != 255), the
+        OpenGL-axes camera-to-world pose and the mask's [cmin, rmin, cmax, rmax] box."""
+        img = _imread_rgb(rgb_path)
+        fg = np.all(img != 255, axis=-1)
+        ys, xs = np.nonzero(fg.any(axis=1))[0], np.nonzero(fg.any(axis=0))[0]
+        if ys.size == 0:
+            raise RuntimeError("Bad image at %s (no foreground pixel)" % rgb_path)
+        box = torch.tensor([xs[0], ys[0], xs[-1], ys[-1]], dtype=torch.float32)
+        c2w = torch.from_numpy(np.loadtxt(pose_path, dtype=np.float32).reshape(4, 4)) @ self._coord_trans
+        mask = fg[..., None].astype(np.uint8) * 255
+        return image_to_tensor_balanced(img), mask_to_tensor(mask), c2w, box
+
     def __getitem__(self, index):
         intrin_path = self.intrins[index]
-        dir_path = os.path.dirname(intrin_path)
-        rgb_paths = sorted(glob.glob(os.path.join(dir_path, "rgb", "*")))
-        pose_paths = sorted(glob.glob(os.path.join(dir_path, "pose", "*")))
+        obj_dir = os.path.dirname(intrin_path)
+        rgb_paths = sorted(glob.glob(os.path.join(obj_dir, "rgb", "*")))
+        pose_paths = sorted(glob.glob(os.path.join(obj_dir, "pose", "*")))
         assert len(rgb_paths) == len(pose_paths)
-        with open(intrin_path, "r") as f:
-            lines = f.readlines()
-            focal, cx, cy, _ = map(float, lines[0].split())
-            height, width = map(int, lines[-1].split())   # noqa: F841 (read as the reference does)
-
-        imgs, poses, masks, bboxes = [], [], [], []
-        for rgb_path, pose_path in zip(rgb_paths, pose_paths):
-            img = _imread_rgb(rgb_path)
-            mask = (img != 255).all(axis=-1)[..., None].astype(np.uint8) * 255
-            pose = torch.from_numpy(np.loadtxt(pose_path, dtype=np.float32).reshape(4, 4))
-            pose = pose @ self._coord_trans
-            rows = np.any(mask, axis=1)
-            cols = np.any(mask, axis=0)
-            rnz, cnz = np.where(rows)[0], np.where(cols)[0]
-            if len(rnz) == 0:
-                raise RuntimeError("Bad image at %s (no foreground pixel)" % rgb_path)
-            rmin, rmax = rnz[[0, -1]]
-            cmin, cmax = cnz[[0, -1]]
-            imgs.append(image_to_tensor_balanced(img))
-            masks.append(mask_to_tensor(mask))
-            poses.append(pose)
-            bboxes.append(torch.tensor([cmin, rmin, cmax, rmax], dtype=torch.float32))
-
-        all_imgs = torch.stack(imgs)
-        all_poses = torch.stack(poses)
-        all_masks = torch.stack(masks)
-        all_bboxes = torch.stack(bboxes)
-        if tuple(all_imgs.shape[-2:]) != self.image_size:
-            scale = self.image_size[0] / all_imgs.shape[-2]
-            focal *= scale
-            cx *= scale
-            cy *= scale
-            all_bboxes *= scale
-            all_imgs = F.interpolate(all_imgs, size=self.image_size, mode="area")
-            all_masks = F.interpolate(all_masks, size=self.image_size, mode="area")
+        focal, cx, cy = self._intrinsics(intrin_path)
+        images, masks, poses, boxes = (torch.stack(t) for t in
+                                       zip(*[self._view(r, q) for r, q in zip(rgb_paths, pose_paths)]))
+        if tuple(images.shape[-2:]) != self.image_size:
+            # area-resampled to image_size; intrinsics and boxes follow the row scale
+            k = self.image_size[0] / images.shape[-2]
+            focal, cx, cy, boxes = focal * k, cx * k, cy * k, boxes * k
+            images = F.interpolate(images, size=self.image_size, mode="area")
+            masks = F.interpolate(masks, size=self.image_size, mode="area")
         if self.world_scale != 1.0:
-            focal *= self.world_scale
-            all_poses[:, :3, 3] *= self.world_scale
-        return {
-            "path": dir_path,
-            "img_id": index,
-            "focal": torch.tensor(focal, dtype=torch.float32),
-            "c": torch.tensor([cx, cy], dtype=torch.float32),
-            "images": all_imgs,
-            "masks": all_masks,
-            "bbox": all_bboxes,
-            "poses": all_poses,
-        }
+            focal = focal * self.world_scale
+            poses[:, :3, 3] *= self.world_scale
+        return dict(path=obj_dir, img_id=index, focal=torch.tensor(focal, dtype=torch.float32),
+                    c=torch.tensor([cx, cy], dtype=torch.float32), images=images, masks=masks,
+                    bbox=boxes, poses=poses)
 
 
 def get_split_dataset(dataset_type, datadir, want_split="all", training=True, **kwargs):

@@ -126,14 +126,26 @@ class InferenceTrunk:
                 bias.copy_(-b.running_mean * s if b.bias is None else b.bias - b.running_mean * s)
         self.key = key
 
+    # conv + bias + relu and conv + bias + residual + relu as MIOpen's fused forward ops
+    # (torch.miopen_convolution_relu / _add_relu); False: F.conv2d + in-place relu / add
+    fused = True
+
     def trunk(self, x):
         enc = self.owner()
         m = enc.model
         f = self.folded
+        fused = self.fused
 
-        def conv(c, x, relu=True):
+        def conv(c, x, relu=True, add=None):
             w, b = f[id(c)]
+            if fused and relu:
+                if add is None:
+                    return torch.miopen_convolution_relu(x, w, b, c.stride, c.padding, c.dilation, c.groups)
+                return torch.miopen_convolution_add_relu(x, w, add, 1.0, b, c.stride, c.padding, c.dilation,
+                                                         c.groups)
             y = F.conv2d(x, w, b, c.stride, c.padding, c.dilation, c.groups)
+            if add is not None:
+                y = y.add_(add)
             return torch.relu_(y) if relu else y
 
         x = conv(m.conv1, x)
@@ -143,8 +155,7 @@ class InferenceTrunk:
         for layer in self.layers:
             for blk in layer:
                 idt = x if blk.downsample is None else conv(blk.downsample[0], x, relu=False)
-                y = conv(blk.conv2, conv(blk.conv1, x), relu=False)
-                x = torch.relu_(y.add_(idt))
+                x = conv(blk.conv2, conv(blk.conv1, x), add=idt)
             maps.append(x)
         return _latent_channels_last(maps)
 
@@ -153,8 +164,14 @@ class InferenceTrunk:
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):   # MIOpen solver search and allocator warm-up, outside the capture
-            for _ in range(2):
+            try:
                 self.trunk(xin)
+            except RuntimeError as e:   # a fused op MIOpen refuses for this shape: the unfused form
+                if not self.fused:
+                    raise
+                warnings.warn("pnr: MIOpen fused conv+relu unavailable (%s); unfused convolutions" % e)
+                self.fused = False
+            self.trunk(xin)
         torch.cuda.current_stream(self.device).wait_stream(side)
         graph = torch.cuda.CUDAGraph()
         try:
