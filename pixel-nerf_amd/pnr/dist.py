@@ -154,7 +154,9 @@ class GradReducer:
         self.late = []         # params accumulated again after their bucket was launched
 
     def _ready(self, p):
-        if not self.armed:
+        if not self.armed or p.grad is None:
+            # None: the engine runs post-accumulate hooks also for a parameter whose backward
+            # returned no gradient; whoever sets .grad later runs the hook again
             return
         if id(p) in self.launched:
             if all(q is not p for q in self.late):
