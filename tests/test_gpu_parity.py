@@ -597,6 +597,45 @@ def test_render_large_batch_properties():
     assert out.fine.weights.shape == (1, B, 128)
 
 
+def test_render_repeatable_under_memory_contention():
+    """The shipped lin_z stage (stage_proj_runs: run-deduplicated corner-row loads blended into
+    the LDS stage) under slow loads: the round-3 stagger's nondeterminism appeared only while the
+    stage's loads competed with a weight stream (DESIGN §3, "The round-3 stagger's
+    nondeterminism").  Here the cfg2 render (4096 rays x (64 + 64), projected latent) runs once
+    alone and twice while a side stream streams 2 x 1 GiB copies through HBM / L2 beside it (the
+    copy's workgroups take CUs first, k_point_mlp's persistent workgroups fill the rest and load
+    under that traffic); all three are bitwise identical."""
+    sd = synth.pixelnerf_state(1)
+    sc = synth.scene_srn(seed=0, n_rays=4096, pick="all")
+    net = PixelNeRFNet(model_conf())
+    net.load_state_dict(sd, strict=False)
+    net = net.to(DEV).eval()
+    assert net.use_latent_proj
+    net.encode_latent(sc["latent"].to(DEV), sc["poses"].to(DEV), sc["focal"].to(DEV), (128, 128))
+    r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=True)
+    rays = sc["rays"].to(DEV)[None]
+    src = torch.empty(1 << 28, device=DEV)
+    dst = torch.empty_like(src)
+    side = torch.cuda.Stream()
+    outs = []
+    with torch.no_grad():
+        for noisy in (False, True, True):
+            torch.manual_seed(5)
+            torch.cuda.synchronize()
+            if noisy:
+                with torch.cuda.stream(side):
+                    for _ in range(2):
+                        dst.copy_(src)
+            out = r(net, rays, want_weights=True)
+            outs.append({p: (out[p].rgb.clone(), out[p].depth.clone(), out[p].weights.clone())
+                         for p in ("coarse", "fine")})
+            torch.cuda.synchronize()
+    for o in outs[1:]:
+        for p in ("coarse", "fine"):
+            for a, b in zip(outs[0][p], o[p]):
+                assert torch.equal(a, b), p
+
+
 def test_full_frame_dtu_ns3_properties_and_fixture_rows():
     """cfg4 at full size: one 400x300 frame (120,000 rays) with NS = 3 source views and the
     real 150x200 latent per view (the multi-view mean path).  The fixture fw_dtu_ns3 holds
