@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 4   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic) */
+#define PNR_ABI_VERSION 5   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
+                               5: pnr_latent_channels_last_nhwc */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -309,6 +310,14 @@ int pnr_latent_channels_last(const float *const *maps, const int32_t *channels,
                              const int32_t *heights, const int32_t *widths, int32_t n_maps,
                              int32_t n_images, float *latent_cl, int32_t out_h, int32_t out_w,
                              pnr_stream_t stream);
+
+/* pnr_latent_channels_last with every maps[k] channels-last, (n_images, heights[k], widths[k],
+ * channels[k]) (the trunk's maps when its convolutions run in channels-last memory format):
+ * the same arithmetic and output (ABI 5). */
+int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *channels,
+                                  const int32_t *heights, const int32_t *widths, int32_t n_maps,
+                                  int32_t n_images, float *latent_cl, int32_t out_h, int32_t out_w,
+                                  pnr_stream_t stream);
 
 /* ---- training (autograd over the ray march) ------------ */
 /* Floats of the activation save of pnr_render_points for n_points rows; call it with

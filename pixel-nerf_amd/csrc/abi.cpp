@@ -35,7 +35,7 @@ size_t wgrad_workspace_bytes(int, int64_t);
 int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
                  hipStream_t, int arith);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
-                     int, int, hipStream_t);
+                     int, int, bool, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
                          const float *, const float *, float *, float *, hipStream_t);
 int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, int, const float *, const float *,
@@ -586,7 +586,18 @@ int pnr_latent_channels_last(const float *const *maps, const int32_t *channels, 
     if (!maps || !channels || !heights || !widths || !latent_cl)
         return fail(PNR_ERR_INVALID, "pnr_latent_channels_last: NULL");
     if (n_images < 0 || out_h < 1 || out_w < 1) return fail(PNR_ERR_INVALID, "pnr_latent_channels_last: bad sizes");
-    return launch_latent_cl(maps, channels, heights, widths, n_maps, n_images, latent_cl, out_h, out_w,
+    return launch_latent_cl(maps, channels, heights, widths, n_maps, n_images, latent_cl, out_h, out_w, false,
+                            (hipStream_t)stream);
+}
+
+int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *channels, const int32_t *heights,
+                                  const int32_t *widths, int32_t n_maps, int32_t n_images, float *latent_cl,
+                                  int32_t out_h, int32_t out_w, pnr_stream_t stream) {
+    if (!maps || !channels || !heights || !widths || !latent_cl)
+        return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_nhwc: NULL");
+    if (n_images < 0 || out_h < 1 || out_w < 1)
+        return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_nhwc: bad sizes");
+    return launch_latent_cl(maps, channels, heights, widths, n_maps, n_images, latent_cl, out_h, out_w, true,
                             (hipStream_t)stream);
 }
 

@@ -4,7 +4,9 @@
 // feature map (conv1, layer1..layer3, NCHW) is bilinearly upsampled to the first map's
 // size (align_corners = True) and concatenated along channels.  The ray march consumes
 // the latent channels-LAST, so this kernel writes (N, H_l, W_l, sum C) directly: no
-// NCHW concat and no transpose copy.  Arithmetic as torch's CPU upsample_bilinear2d:
+// NCHW concat and no transpose copy.  The maps may also be channels-last (NHWC) themselves,
+// the trunk's layout when its convolutions run in channels-last memory format: consecutive
+// threads then read consecutive channels of one source pixel.  Arithmetic as torch's CPU upsample_bilinear2d:
 //   scale = (in - 1) / (out - 1) (float), src = scale * dst, i0 = (int) src,
 //   l1 = src - i0, l0 = 1 - l1, i1 = i0 + (i0 < in - 1),
 //   out = l0h (l0w v00 + l1w v01) + l1h (l0w v10 + l1w v11)
@@ -30,6 +32,7 @@ __device__ __forceinline__ void src_index(int in, int out, int dst, int &i0, int
     l0 = sub_rn(1.f, l1);
 }
 
+template <bool NHWC>
 __global__ __launch_bounds__(256) void k_latent_cl(LatentMaps m, int64_t n_out, int out_h, int out_w,
                                                    float *__restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -47,13 +50,15 @@ __global__ __launch_bounds__(256) void k_latent_cl(LatentMaps m, int64_t n_out, 
         if (j < m.n_maps && c >= m.c0[j]) k = j;
     const int cc = c - m.c0[k], hm = m.h[k], wm = m.w[k];
     const int cm = m.c0[k + 1] - m.c0[k];
-    const float *src = m.ptr[k] + ((n * cm + cc) * (int64_t)hm) * wm;
+    // element (y, x) of this channel: NCHW plane pitch 1, NHWC pixel pitch cm
+    const float *src = NHWC ? m.ptr[k] + n * (int64_t)hm * wm * cm + cc : m.ptr[k] + ((n * cm + cc) * (int64_t)hm) * wm;
+    const int64_t px = NHWC ? cm : 1;
     int y0, y1, x0, x1;
     float ly0, ly1, lx0, lx1;
     src_index(hm, out_h, y, y0, y1, ly0, ly1);
     src_index(wm, out_w, x, x0, x1, lx0, lx1);
-    const float v00 = src[(int64_t)y0 * wm + x0], v01 = src[(int64_t)y0 * wm + x1];
-    const float v10 = src[(int64_t)y1 * wm + x0], v11 = src[(int64_t)y1 * wm + x1];
+    const float v00 = src[((int64_t)y0 * wm + x0) * px], v01 = src[((int64_t)y0 * wm + x1) * px];
+    const float v10 = src[((int64_t)y1 * wm + x0) * px], v11 = src[((int64_t)y1 * wm + x1) * px];
     const float top = add_rn(mul_rn(lx0, v00), mul_rn(lx1, v01));
     const float bot = add_rn(mul_rn(lx0, v10), mul_rn(lx1, v11));
     out[i] = add_rn(mul_rn(ly0, top), mul_rn(ly1, bot));
@@ -61,7 +66,7 @@ __global__ __launch_bounds__(256) void k_latent_cl(LatentMaps m, int64_t n_out, 
 
 int launch_latent_cl(const float *const *maps, const int32_t *channels, const int32_t *heights,
                      const int32_t *widths, int n_maps, int n_images, float *latent_cl, int out_h, int out_w,
-                     hipStream_t st) {
+                     bool nhwc, hipStream_t st) {
     if (n_maps < 1 || n_maps > MAX_MAPS) return fail(PNR_ERR_UNSUPPORTED, "latent: 1..8 feature maps");
     LatentMaps m = {};
     m.n_maps = n_maps;
@@ -76,8 +81,9 @@ int launch_latent_cl(const float *const *maps, const int32_t *channels, const in
     }
     const int64_t n_out = (int64_t)n_images * out_h * out_w * m.c0[n_maps];
     if (n_out == 0) return PNR_OK;
-    hipLaunchKernelGGL(k_latent_cl, dim3((unsigned)((n_out + 255) / 256)), dim3(256), 0, st, m, n_out, out_h,
-                       out_w, latent_cl);
+    const dim3 grid((unsigned)((n_out + 255) / 256));
+    if (nhwc) hipLaunchKernelGGL(k_latent_cl<true>, grid, dim3(256), 0, st, m, n_out, out_h, out_w, latent_cl);
+    else hipLaunchKernelGGL(k_latent_cl<false>, grid, dim3(256), 0, st, m, n_out, out_h, out_w, latent_cl);
     return launch_ok("latent_cl") ? PNR_OK : PNR_ERR_HIP;
 }
 

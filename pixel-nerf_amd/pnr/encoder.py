@@ -23,10 +23,18 @@ from .consts import device_const
 __all__ = ["SpatialEncoder", "ImageEncoder", "resnet34_trunk"]
 
 
+def _nhwc(maps):
+    """Every map channels-last in memory (the trunk's convolutions in channels-last format)."""
+    return all(t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous() for t in maps)
+
+
 def _latent_channels_last(maps):
     from . import _lib
 
-    maps = [t.contiguous().float() for t in maps]
+    maps = [t.float() for t in maps]
+    nhwc = _nhwc(maps)
+    if not nhwc:
+        maps = [t.contiguous() for t in maps]
     n, (h, w) = maps[0].shape[0], maps[0].shape[-2:]
     c_total = sum(t.shape[1] for t in maps)
     out = torch.empty(n, h, w, c_total, dtype=torch.float32, device=maps[0].device)
@@ -35,9 +43,9 @@ def _latent_channels_last(maps):
     ch = (ctypes.c_int32 * k)(*[t.shape[1] for t in maps])
     hs = (ctypes.c_int32 * k)(*[t.shape[2] for t in maps])
     ws = (ctypes.c_int32 * k)(*[t.shape[3] for t in maps])
-    _lib.check(_lib.load().pnr_latent_channels_last(ptrs, ch, hs, ws, k, n, _lib.ptr(out), h, w,
-                                                     _lib.stream_of(out.device)),
-               "pnr_latent_channels_last")
+    name = "pnr_latent_channels_last_nhwc" if nhwc else "pnr_latent_channels_last"
+    _lib.check(getattr(_lib.load(), name)(ptrs, ch, hs, ws, k, n, _lib.ptr(out), h, w, _lib.stream_of(out.device)),
+               name)
     return out
 
 
@@ -50,6 +58,7 @@ class LatentChannelsLast(torch.autograd.Function):
     @staticmethod
     def forward(ctx, *maps):
         ctx.shapes = [tuple(t.shape) for t in maps]
+        ctx.nhwc = _nhwc(maps)
         return _latent_channels_last(maps)
 
     @staticmethod
@@ -61,7 +70,8 @@ class LatentChannelsLast(torch.autograd.Function):
             gi = gn[:, c0:c0 + shp[1]]
             c0 += shp[1]
             if tuple(shp[-2:]) == (h, w):
-                grads.append(gi.contiguous())
+                # the map's own layout (a channels-last trunk's backward convolutions take NHWC)
+                grads.append(gi.contiguous(memory_format=torch.channels_last if ctx.nhwc else torch.contiguous_format))
             else:
                 grads.append(torch.ops.aten.upsample_bilinear2d_backward(
                     gi, [h, w], list(shp), True, None, None))
@@ -127,8 +137,11 @@ class InferenceTrunk:
         self.key = key
 
     # conv + bias + relu and conv + bias + residual + relu as MIOpen's fused forward ops
-    # (torch.miopen_convolution_relu / _add_relu); False: F.conv2d + in-place relu / add
-    fused = True
+    # (torch.miopen_convolution_relu / _add_relu); False: F.conv2d + in-place relu / add.
+    # Off: on the channels-last trunk F.conv2d is fastest (cfg3 encode 0.51 ms against 0.58 ms
+    # NCHW and 0.60 ms fused NCHW; the fused ops on NHWC take 44 ms, a fallback kernel:
+    # profiles/r4k/encode_ab_cl.txt), so they are never used on channels-last input
+    fused = False
 
     def trunk(self, x):
         enc = self.owner()
@@ -148,6 +161,7 @@ class InferenceTrunk:
                 y = y.add_(add)
             return torch.relu_(y) if relu else y
 
+        fused = fused and not x.is_contiguous(memory_format=torch.channels_last)
         x = conv(m.conv1, x)
         maps = [x]
         if self.layers and enc.use_first_pool:
@@ -283,7 +297,10 @@ class SpatialEncoder(nn.Module):
         # index(), PixelNeRFNet.fused_conf_reason)
         self.feature_scale = feature_scale
         self.use_first_pool = use_first_pool
-        self.model = resnet34_trunk(pretrained, _norm_layer(norm_type))
+        # channels-last (NHWC) trunk: MIOpen's NHWC convolutions, without the NCHW<->NHWC
+        # transposes it otherwise wraps around them; the eval encode 0.58 -> 0.51 ms (cfg3) and the
+        # cfg5 training step 14.8 -> 14.4 ms (profiles/r4k).  Same parameters and state-dict values.
+        self.model = resnet34_trunk(pretrained, _norm_layer(norm_type)).to(memory_format=torch.channels_last)
         self.latent_size = [0, 64, 128, 256, 512, 1024][num_layers]
         self.num_layers = num_layers
         self.index_interp = index_interp
@@ -312,7 +329,7 @@ class SpatialEncoder(nn.Module):
                               mode="bilinear" if self.feature_scale > 1.0 else "area",
                               align_corners=True if self.feature_scale > 1.0 else None,
                               recompute_scale_factor=True)
-        x = x.to(device=self.latent.device)
+        x = x.to(device=self.latent.device).contiguous(memory_format=torch.channels_last)
         if self._use_infer(x):
             return self.set_latent_cl(self._infer.run(x))
         m = self.model

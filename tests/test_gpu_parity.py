@@ -753,17 +753,21 @@ def test_frame_render_matches_reference_gen_video():
 
 
 # --------------------------------------------------------------- encoder --
-def test_latent_channels_last_backward_matches_torch_autograd():
+@pytest.mark.parametrize("nhwc", [False, True])
+def test_latent_channels_last_backward_matches_torch_autograd(nhwc):
     """LatentChannelsLast (the training encoder's upsample + concat, encoder.py:150-160, as one
     HIP kernel) against autograd of F.interpolate(align_corners) + torch.cat + the
-    channels-last permute: forward and the gradient of every trunk map."""
+    channels-last permute: forward and the gradient of every trunk map, with NCHW maps and with
+    channels-last maps (pnr_latent_channels_last_nhwc, the channels-last trunk's)."""
     import torch.nn.functional as F
 
     from pnr.encoder import LatentChannelsLast
 
     gen = torch.Generator(device="cpu").manual_seed(5)
     shapes = [(2, 64, 32, 40), (2, 64, 16, 20), (2, 128, 8, 10), (2, 256, 4, 5)]
-    maps = [torch.randn(sh, generator=gen).to(DEV).requires_grad_(True) for sh in shapes]
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
+    maps = [torch.randn(sh, generator=gen).to(DEV).contiguous(memory_format=fmt).requires_grad_(True)
+            for sh in shapes]
     out = LatentChannelsLast.apply(*maps)
     ref = torch.cat([F.interpolate(m, (32, 40), mode="bilinear", align_corners=True) for m in maps],
                     1).permute(0, 2, 3, 1)
@@ -776,10 +780,12 @@ def test_latent_channels_last_backward_matches_torch_autograd():
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item(), (a - b).abs().max().item()
 
 
-def test_latent_channels_last_matches_torch_upsample_concat():
-    """pnr_latent_channels_last (encoder.py:150-160 tail) vs the
-    reference's F.interpolate(bilinear, align_corners=True) + cat, transposed; and a no-grad
-    SpatialEncoder.forward on the device takes that path (latent_cl written directly)."""
+@pytest.mark.parametrize("nhwc", [False, True])
+def test_latent_channels_last_matches_torch_upsample_concat(nhwc):
+    """pnr_latent_channels_last (encoder.py:150-160 tail; NCHW maps) and
+    pnr_latent_channels_last_nhwc (channels-last maps) vs the reference's F.interpolate(bilinear,
+    align_corners=True) + cat, transposed; and a no-grad SpatialEncoder.forward on the device
+    takes that path (latent_cl written directly)."""
     import torch.nn.functional as F
     from pnr.encoder import SpatialEncoder
 
@@ -790,8 +796,9 @@ def test_latent_channels_last_matches_torch_upsample_concat():
     ref = torch.cat([F.interpolate(t, (48, 56), mode="bilinear", align_corners=True) for t in maps], 1)
     ref = ref.permute(0, 2, 3, 1).contiguous()
     enc = SpatialEncoder(pretrained=False).to(DEV)
+    fmt = torch.channels_last if nhwc else torch.contiguous_format
     with torch.no_grad():
-        enc.set_latent_maps([t.to(DEV) for t in maps])
+        enc.set_latent_maps([t.to(DEV).contiguous(memory_format=fmt) for t in maps])
     got = enc.latent_cl.cpu()
     assert got.shape == ref.shape
     torch.testing.assert_close(got, ref, atol=1e-5, rtol=0)   # O(1) values: a few ulps

@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.pnr_abi_version() == 4
+    assert lib.pnr_abi_version() == 5
     # an invalid call fails with a message, without touching the GPU
     rc = lib.pnr_composite(None, None, None, 4, 0, 0, None, None, None, None)
     assert rc == -1
