@@ -329,7 +329,9 @@ class SpatialEncoder(nn.Module):
                               mode="bilinear" if self.feature_scale > 1.0 else "area",
                               align_corners=True if self.feature_scale > 1.0 else None,
                               recompute_scale_factor=True)
-        x = x.to(device=self.latent.device).contiguous(memory_format=torch.channels_last)
+        x = x.to(device=self.latent.device)
+        if x.dim() == 4:   # the trunk's channels-last layout (a no-op for a channels-last input)
+            x = x.contiguous(memory_format=torch.channels_last)
         if self._use_infer(x):
             return self.set_latent_cl(self._infer.run(x))
         m = self.model

@@ -56,4 +56,3 @@ for rnd in range(2):
             print("%-7s %-4s %.4f ms per encode   max|d| / max|ref| %.2e   graph %s fused %s" % (
                 form, "nhwc" if cl else "nchw", ms, d, used is not None and used.use_graph and bool(used.graphs),
                 used is not None and used.fused), flush=True)
-InferenceTrunk.fused = True
