@@ -8,6 +8,7 @@ These mirror the semantics (not the code) of the reference's ``src/util/util.py`
 * ``gen_rays``            — util.py:238-276 (rays ``[o(3), d(3), near, far]``)
 * ``pose_spherical``      — util.py:309-323 (NeRF 360° camera path)
 * ``psnr``                — util.py:474-481
+* ``bbox_sample``         — util.py:220-235 (the training step's pixel picks inside object boxes)
 
 They run on whatever device their inputs live on; none of them is on the
 per-point hot path (ray generation on device is SURVEY §8(f) rank 1).
@@ -25,6 +26,7 @@ __all__ = [
     "pose_spherical",
     "psnr",
     "batched_index_select_nd",
+    "bbox_sample",
 ]
 
 
@@ -49,6 +51,18 @@ def combine_interleaved(t, inner_dims=(1,), agg_type="average"):
 def batched_index_select_nd(t, inds):
     """Gather along dim 1 of a batched tensor (util.py:33-42)."""
     return t.gather(1, inds[(...,) + (None,) * (len(t.shape) - 2)].expand(-1, -1, *t.shape[2:]))
+
+
+def bbox_sample(bboxes, num_pix):
+    """(num_pix, 3) pixel picks [view, row, col] inside per-view boxes (util.py:220-235):
+    ``bboxes`` (NV, 4) = [cmin, rmin, cmax, rmax] (inclusive).  Draws from torch's default host
+    generator in the reference's order -- the view ids, then the columns, then the rows -- so a
+    seeded call picks the reference's pixels."""
+    view = torch.randint(0, bboxes.shape[0], (num_pix,))
+    box = bboxes[view]
+    col = (torch.rand(num_pix) * (box[:, 2] + 1 - box[:, 0]) + box[:, 0]).long()
+    row = (torch.rand(num_pix) * (box[:, 3] + 1 - box[:, 1]) + box[:, 1]).long()
+    return torch.stack((view, row, col), dim=-1)
 
 
 def unproj_map(width, height, f, c=None, device="cpu"):

@@ -436,6 +436,21 @@ def gen_rays_case(name):
                      rays2=r2.numpy())
 
 
+def bbox_sample_case(name):
+    """util.bbox_sample (util.py:220-235) from a seeded host generator: float boxes as the SRN
+    loader makes them (and the area-resampled, non-integer ones), and integer boxes."""
+    import util
+
+    boxes = torch.tensor([[10.0, 12.0, 90.0, 100.0], [0.0, 0.0, 127.0, 127.0], [40.5, 33.25, 60.75, 70.5]])
+    iboxes = torch.tensor([[3, 4, 20, 9], [0, 0, 0, 0]])
+    torch.manual_seed(2024)
+    pix = util.bbox_sample(boxes, 300)
+    torch.manual_seed(7)
+    ipix = util.bbox_sample(iboxes, 64)
+    cfg = dict(name=name, seed=2024, num_pix=300, iseed=7, inum_pix=64)
+    return cfg, dict(boxes=boxes.numpy(), pix=pix.numpy(), iboxes=iboxes.numpy(), ipix=ipix.numpy())
+
+
 def save(cfg, arrays):
     path = os.path.join(HERE, cfg["name"] + ".npz")
     np.savez_compressed(path, config=np.array(json.dumps(cfg)), **arrays)
@@ -518,6 +533,8 @@ def main():
                           n_coarse=64, n_fine=64, n_fine_depth=0, white_bkgd=True, rng_seed=11))
     if want("train_step"):
         save(*train_case("train_step"))
+    if want("bbox_sample"):
+        save(*bbox_sample_case("bbox_sample"))
     if want("gen_rays"):
         save(*gen_rays_case("gen_rays"))
     if want("frame32"):
