@@ -256,3 +256,57 @@ def test_eval_and_video_scripts_end_to_end(tmp_path):
     frames = sorted(os.listdir(tmp_path / "vis" / "synthnet" / "videot0001_v001"))
     assert frames == ["0000.png", "0001.png", "0002.png"]
     assert (tmp_path / "vis" / "synthnet" / "videot0001_v001.gif").exists()
+
+
+@pytest.mark.gpu
+def test_eval_script_density_grid_and_compare(tmp_path):
+    """scripts/eval.py (eval/eval.py): the density grid of each object (the point query over a
+    res^3 grid in 65,536-point chunks) equals PixelNeRFNet.forward at the same points in this
+    process, and --compare writes eval.py's finish.txt line per object."""
+    import os
+    import subprocess
+    import sys
+
+    from pnr import synth
+    from pnr.conf import parse_file
+    from pnr.models import make_model
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    g = _golden()
+    root = write_srn_dir(str(tmp_path), g)
+    (tmp_path / "exp.conf").write_text(CLI_CONF)
+    ck = tmp_path / "ck" / "synthnet"
+    ck.mkdir(parents=True)
+    net = make_model(parse_file(str(tmp_path / "exp.conf"))["model"])
+    full = net.state_dict()
+    full.update(synth.pixelnerf_state(2))
+    torch.save(full, str(ck / "pixel_nerf_latest"))
+    res = 20
+    r = subprocess.run([sys.executable, os.path.join(repo, "scripts", "eval.py"), "-c", str(tmp_path / "exp.conf"),
+                        "-D", root, "-n", "synthnet", "--checkpoints_path", str(tmp_path / "ck"), "--split", "test",
+                        "-P", "0 1", "--mesh_res", str(res), "--compare", "-O", str(tmp_path / "out")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    dset = get_split_dataset("srn", root, want_split="test", training=False)
+    lines = (tmp_path / "out" / "finish.txt").read_text().strip().splitlines()
+    assert len(lines) == len(dset)
+    dev = torch.device("cuda")
+    net.load_state_dict(full)
+    net = net.to(dev).eval()
+    for i in range(len(dset)):
+        data = dset[i]
+        name = os.path.basename(data["path"])
+        sig = np.load(str(tmp_path / "out" / name / (name + "_sigma.npy")))
+        assert sig.shape == (res, res, res) and np.isfinite(sig).all() and (sig >= 0).all()
+        fields = lines[i].split()
+        assert fields[0] == name and fields[3] == "1" and np.isfinite(float(fields[1]))
+        focal = torch.as_tensor(data["focal"], dtype=torch.float32)[None].to(dev)
+        with torch.no_grad():
+            net.encode(data["images"][:2].to(dev)[None], data["poses"][:2].to(dev)[None], focal,
+                       c=data["c"].to(dev)[None])
+            grid = torch.linspace(-1, 1, res, device=dev)
+            idx = torch.tensor([[0, 0, 0], [3, 7, 11], [19, 19, 19], [10, 2, 17]])
+            pts = grid[idx.to(dev)]
+            got = torch.relu(net(pts[None], coarse=True, viewdirs=torch.zeros_like(pts[None]))[0, :, 3]).cpu()
+        want = torch.from_numpy(sig[idx[:, 0], idx[:, 1], idx[:, 2]])
+        assert torch.equal(got, want), (got, want)
