@@ -540,6 +540,42 @@ def _time_render(net, renderer, rays, chunk, passes=2):
     return (time.perf_counter() - t0) / passes
 
 
+def density_grid_leg(net, dev, precision, latent_proj, res=256, chunk=65536):
+    """eval/eval.py's density grid (eval.py:93-103; scripts/eval.py): relu(sigma) of the coarse net
+    at res^3 points over [-1, 1]^3 through PixelNeRFNet.forward (the point query, SURVEY §8(a)
+    a17) in the caller's 65,536-point chunks.  Timed with events around the whole pass (res^3 /
+    chunk launches with their host glue), so its rate includes each launch's ramp and tail."""
+    grid = torch.linspace(-1, 1, res, device=dev)
+    pts = torch.stack(torch.meshgrid(grid, grid, grid, indexing="ij"), -1).reshape(-1, 3)
+    vd = torch.zeros(1, chunk, 3, device=dev)
+    sig = torch.empty(pts.shape[0], device=dev)
+
+    def grid_pass():
+        for i in range(0, pts.shape[0], chunk):
+            p = pts[i:i + chunk][None]
+            sig[i:i + chunk] = net(p, coarse=True, viewdirs=vd[:, :p.shape[1]])[0, :, 3]
+
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.no_grad():
+        grid_pass()
+        torch.cuda.synchronize(dev)
+        e0.record()
+        grid_pass()
+        e1.record()
+        torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1)
+    assert bool(torch.isfinite(sig).all())
+    n = pts.shape[0]
+    flop = n * flop_per_point(1, latent_proj)
+    peak = PEAK_BY_PRECISION[precision][0]
+    return dict(points_per_s=round(n / ms * 1e3, 1), ms_per_grid=round(ms, 3), points=n, chunk=chunk,
+                workload="eval.py density grid: %d^3 points of the coarse net, %d-point point-query calls" % (res, chunk),
+                roofline=dict(achieved=round(flop / (ms * 1e-3) / 1e12, 2), peak=round(peak, 1),
+                              frac=round(flop / (ms * 1e-3) / 1e12 / peak, 4),
+                              unit="TFLOP/s (fp32-equivalent: %d FLOP per point x points / the whole pass, "
+                                   "launch ramps and host glue included)" % flop_per_point(1, latent_proj)))
+
+
 def extra_configs(dev, precision, latent_proj=True, probe=None, oracle_rays=64):
     """Other SURVEY §8(d) workloads on 1 GPU (informational, not `value`): cfg2 with the
     shipped conf (64 + 32 incl. 16 depth samples), cfg2 as eval_approx.py --coarse renders it
@@ -571,6 +607,7 @@ def extra_configs(dev, precision, latent_proj=True, probe=None, oracle_rays=64):
     s = _time_render(net, r, rays, CHUNK)
     res["cfg2_coarse_as_fine_64_128"] = dict(rays_per_s=round(rays.shape[0] / s, 1),
                                              ms_per_frame=round(s * 1e3, 3))
+    res["eval_density_grid_256"] = density_grid_leg(net, dev, precision, latent_proj)
     sc = synth.scene_multiview(seed=8, n_views=3, n_rays=1)
     net = make(synth.latent(8, 3, 512, 150, 200), sc["poses"][None], sc["focal"][None], (400, 300),
                c=sc["c"][None])
