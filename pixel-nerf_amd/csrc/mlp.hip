@@ -57,7 +57,7 @@ struct Layout {
     int prec;                      // 0 = f32 MFMA, 6 / 9 = split-bf16 products, 3 = scaled f16
     int n_linz, n_l512, n_blocks, ncomb, d_in, d_out, pe_n;
     int64_t layer_floats;
-    int64_t off_lin_in, off_l512, off_lin_out, off_bias, nbias, total;
+    int64_t off_lin_in, off_l512, off_lin_out, off_bias, nbias, off_out32, total;
 };
 
 inline Layout make_layout(const pnr_mlp_desc &d) {
@@ -76,7 +76,9 @@ inline Layout make_layout(const pnr_mlp_desc &d) {
     L.off_lin_out = L.off_l512 + (int64_t)L.n_l512 * L.layer_floats;
     L.off_bias = L.off_lin_out + (int64_t)NKB * 256;
     L.nbias = (int64_t)(1 + L.n_l512) * H + 16;
-    L.total = ((L.off_bias + L.nbias + 63) / 64) * 64;
+    // PREC 3: lin_out's weights in fp32 as [input channel][4 outputs] (the VALU head, k_point_mlp)
+    L.off_out32 = ((L.off_bias + L.nbias + 63) / 64) * 64;
+    L.total = L.off_out32 + (L.prec == 3 ? 4 * H : 0);
     return L;
 }
 
@@ -98,13 +100,11 @@ __global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
     if (i >= L.total) return;
     float v = 0.0f;
     if (i < HDR) {
-        if (i >= HDR_ESCALE && L.prec == 3) return;   // written by k_layer_escale
+        if (i >= HDR_ESCALE && i < HDR_ESCALE + 1 + L.n_l512 && L.prec == 3) return;   // k_layer_escale's
         if (i < 16 && i < L.pe_n) v = s.pe_f[i];
         else if (i >= 16 && i < 32 && (i - 16) < L.pe_n) v = s.pe_p[i - 16];
     } else if (i < L.off_lin_out && L.prec) {
         return;   // written by k_pack_split / k_pack_f16
-    } else if (i < L.off_bias && L.prec == 3) {
-        return;   // lin_out: written by k_pack_f16
     } else if (i < L.off_l512) {
         const int e = (int)(i - L.off_lin_in);
         const int kb = e / KB_FLOATS, rt = (e / 256) % NRT, lane = (e >> 2) & 63, j = e & 3;
@@ -122,6 +122,10 @@ __global__ void k_pack(PackSrc s, Layout L, float *__restrict__ out) {
         const int kb = e >> 8, lane = (e >> 2) & 63, j = e & 3;
         const int row = lane & 15, col = 16 * kb + 4 * (lane >> 4) + j;
         if (row < L.d_out) v = s.lin_out_w[(int64_t)row * H + col];
+    } else if (i >= L.off_out32) {
+        const int e = (int)(i - L.off_out32);   // [input channel][output]
+        const int ch = e >> 2, j = e & 3;
+        if (j < L.d_out) v = s.lin_out_w[(int64_t)j * H + ch];
     } else {
         const int64_t r = i - L.off_bias;
         const int64_t nb = (int64_t)(1 + L.n_l512) * H;
@@ -197,9 +201,8 @@ __device__ __forceinline__ int scale_exp(float m) {
 // header slot (zeroed by the host first)
 __global__ void k_layer_absmax(PackSrc s, Layout L, float *__restrict__ out) {
     const int layer = (int)blockIdx.y - 1;
-    const bool out_layer = layer == L.n_l512;
-    const float *w = layer < 0 ? s.lin_in_w : (out_layer ? s.lin_out_w : s.w[layer]);
-    const int64_t n = layer < 0 ? (int64_t)H * L.d_in : (out_layer ? (int64_t)L.d_out * H : (int64_t)H * H);
+    const float *w = layer < 0 ? s.lin_in_w : s.w[layer];
+    const int64_t n = layer < 0 ? (int64_t)H * L.d_in : (int64_t)H * H;
     float m = 0.f;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         m = fmaxf(m, fabsf(w[i]));
@@ -215,20 +218,16 @@ __global__ void k_layer_escale(int n_slots, float *__restrict__ out) {
 
 // One thread per (layer, k-step, row tile, lane): 8 weights w * 2^eW, each split
 // into two fp16 parts w0 = f16(w), w1 = f16(w - w0) (RNE), [ks][rt][part][lane][8].
-// lin_out (rows padded to 16): [ks][part][lane][8].
+// (lin_out is not split: the head reads it in fp32 from off_out32.)
 __global__ void k_pack_f16(PackSrc s, Layout L, float *__restrict__ out) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t n_in = (int64_t)KS32_IN * NRT * 64;
     const int64_t n_l = (int64_t)KS32 * NRT * 64;
     const int64_t n_all = n_in + L.n_l512 * n_l;
-    if (t >= n_all + KS32 * 64) return;
+    if (t >= n_all) return;
     int layer, ks, rt, lane;
     float *dst;
-    if (t >= n_all) {
-        layer = L.n_l512;   // lin_out
-        ks = (int)((t - n_all) / 64); rt = 0; lane = (int)((t - n_all) % 64);
-        dst = out + L.off_lin_out + ks * 512 + lane * 4;
-    } else if (t < n_in) {
+    if (t < n_in) {
         layer = -1;
         ks = (int)(t / (NRT * 64)); rt = (int)((t / 64) % NRT); lane = (int)(t % 64);
         dst = out + L.off_lin_in + (int64_t)ks * SKS16_FLOATS + rt * SRT16_FLOATS + lane * 4;
@@ -247,7 +246,6 @@ __global__ void k_pack_f16(PackSrc s, Layout L, float *__restrict__ out) {
         const int col = 32 * ks + 8 * (lane >> 4) + j;
         float w = 0.f;
         if (layer < 0) { if (col < L.d_in) w = s.lin_in_w[(int64_t)row * L.d_in + col]; }
-        else if (layer == L.n_l512) { if (row < L.d_out) w = s.lin_out_w[(int64_t)row * H + col]; }
         else w = s.w[layer][(int64_t)row * H + col];
         const float ws = __builtin_ldexpf(w, ew);
         const _Float16 h0 = (_Float16)ws;
@@ -1223,7 +1221,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // ranges: a slower CU or XCD no longer leaves the rest of the chip idle at the end of
     // the launch.  The next tile is fetched before the head, so the atomic's latency hides.
     int *s_next = reinterpret_cast<int *>(petab + 32);
-    float *hpart = petab + 64;   // PREC 3 head: k-half partials [wave][lane][4] (8 KB)
+    float *hpart = petab + 64;   // PREC 3 head: per-wave partials [wave][column][4] (8 KB)
     // fused march (MARCH): the ray's z [128] | head outputs [128][4], the epilogue scratch,
     // near / far.  (Deferring a ray's epilogue into the next tile, under the SIMD-mate's MFMAs,
     // was measured: the double buffers and the call inside the GEMM region cost more in spills
@@ -1579,40 +1577,54 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier
         pre_publish_sync();
-        publish_relu(x, tile, 2 * L.n_blocks, 0);
-        lds_barrier();
+        if constexpr (PREC == 3) {
+            // no publish: the head reads relu(x) from the accumulators (below); only the
+            // activation save of lin_out's input remains
+            if (a.save) {
+                save_relu(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
+                save_mask(x, sv_mask + PS * 16 * (2 * L.n_blocks), tile, P, wave, lane);
+            }
+        } else {
+            publish_relu(x, tile, 2 * L.n_blocks, 0);
+            lds_barrier();
+        }
         PT(gc, 16);
         PT(gc, 3);
 #ifdef PNR_GEMM_ONLY
         if (0)
 #endif
         if (PREC == 3) {
-            // split-fp16 head: W_out (rows padded to 16) * 2^eW . relu(x) * 2^e_col, the k range
-            // split over the 8 waves: wave w sums column tile w % 4 over k-half w / 4 into LDS;
-            // after the tile's closing barrier waves 0-3 add the two halves and apply the head
-            const int ct = wave % CT, kh = wave / CT;
-            const float *wo = PK() + L.off_lin_out + opaque_lane(lane) * 4 + kh * (KS32 / 2) * 512;
-            const _Float16 *q0 = gc.pb0 + ct * 16 * ROWH + kh * 32 * (KS32 / 2);
-            const _Float16 *q1 = gc.pb1 + ct * 16 * ROWH + kh * 32 * (KS32 / 2);
-            f4 o = {0.f, 0.f, 0.f, 0.f}, o2 = o;
+            // fp32 head straight from the accumulators (resnetfc.py:184 lin_out on relu(x)):
+            // lane (g, cl) holds rows 16 (RTW wave + r) + 4 g + i of column 16 c + cl; it sums
+            // W_out^T (fp32, [channel][output] at off_out32) times relu(x) over its 16 rows, then
+            // over the wave's four lane rows (rows_sum), and lane row g stores column tile g's
+            // partial at hpart[wave][column][output]; after the closing barrier waves 0-3 add the
+            // 8 waves' partials in wave order.  Replaces the last layer's colmax / split publish
+            // and the split-fp16 head GEMM (the k_point_mlp round-4 head change).
+            const int ln = opaque_lane(lane), g4 = ln >> 4, c16 = ln & 15;
+            const float *w32 = PK() + L.off_out32;
+            f4 o[CT];
 #pragma unroll
-            for (int ks = 0; ks < KS32 / 2; ks += 2) {
-                const h8 w0 = *reinterpret_cast<const h8 *>(wo + ks * 512);
-                const h8 w1 = *reinterpret_cast<const h8 *>(wo + ks * 512 + 256);
-                const h8 v0 = *reinterpret_cast<const h8 *>(q0 + 32 * ks);
-                const h8 v1 = *reinterpret_cast<const h8 *>(q1 + 32 * ks);
-                const h8 w2 = *reinterpret_cast<const h8 *>(wo + (ks + 1) * 512);
-                const h8 w3 = *reinterpret_cast<const h8 *>(wo + (ks + 1) * 512 + 256);
-                const h8 v2 = *reinterpret_cast<const h8 *>(q0 + 32 * (ks + 1));
-                const h8 v3 = *reinterpret_cast<const h8 *>(q1 + 32 * (ks + 1));
-                o = mfma_h(w1, v0, o);
-                o2 = mfma_h(w3, v2, o2);
-                o = mfma_h(w0, v1, o);
-                o2 = mfma_h(w2, v3, o2);
-                o = mfma_h(w0, v0, o);
-                o2 = mfma_h(w2, v2, o2);
+            for (int c = 0; c < CT; ++c) o[c] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int r = 0; r < RTW; ++r) {
+                const f4 *wr = reinterpret_cast<const f4 *>(w32 + 4 * (16 * (RTW * wave + r) + 4 * g4));
+                const f4 w[4] = {wr[0], wr[1], wr[2], wr[3]};
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                    const f4 v = relu4(x[r][c]);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) o[c][j] = fmaf(v[i], w[i][j], o[c][j]);
+                }
             }
-            *reinterpret_cast<f4 *>(hpart + (wave * 64 + opaque_lane(lane)) * 4) = o + o2;
+#pragma unroll
+            for (int c = 0; c < CT; ++c)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[c][j] = rows_sum(o[c][j]);
+            const f4 mine = g4 == 0 ? o[0] : g4 == 1 ? o[1] : g4 == 2 ? o[2] : o[3];
+            *reinterpret_cast<f4 *>(hpart + (wave * COLS + 16 * g4 + c16) * 4) = mine;
         } else if (PREC != 3 && wave < CT) {   // wave-uniform: the first CT waves own one column tile each
             const float *wo = PK() + L.off_lin_out + lane * 4;
             const float *bi = inbuf + (16 * wave + cl) * LDS_LD + 4 * g;
@@ -1644,12 +1656,13 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         lds_barrier();   // s_next and the head partials written
         if (PREC == 3 && wave < CT) {   // [sigmoid(rgb), relu(sigma)] of column tile `wave`
             const int ln = opaque_lane(lane), gg = ln >> 4, cc = ln & 15;
-            const f4 h0 = *reinterpret_cast<const f4 *>(hpart + (wave * 64 + ln) * 4);
-            const f4 h1 = *reinterpret_cast<const f4 *>(hpart + ((wave + CT) * 64 + ln) * 4);
-            const int e = ecol[16 * wave + cc] + (int)PK()[HDR_ESCALE + 1 + L.n_l512];
+            const int col = 16 * wave + cc;
+            f4 o = *reinterpret_cast<const f4 *>(hpart + col * 4);
+#pragma unroll
+            for (int w = 1; w < WAVES; ++w) o = o + *reinterpret_cast<const f4 *>(hpart + (w * COLS + col) * 4);
             const f4 b = *reinterpret_cast<const f4 *>(bias + (1 + L.n_l512) * H + 4 * gg);
-            const f4 o = (h0 + h1) * __builtin_ldexpf(1.f, -e) + b;
-            const int64_t po = tile * COLS + 16 * wave + cc;
+            o = o + b;
+            const int64_t po = tile * COLS + col;
             if (gg == 0 && po < a.n_points) {
                 f4 r;
                 r.x = __fdiv_rn(1.f, add_rn(1.f, expf(-o.x)));
@@ -2047,13 +2060,13 @@ int mlp_pack(const pnr_mlp_weights &w, void *packed, size_t bytes, hipStream_t s
     const int64_t n = (int64_t)(mlpk::KS32_IN + L.n_l512 * mlpk::KS32) * mlpk::NRT * 64;
     if (L.prec == PNR_PREC_F16X3) {
         float *hdr = static_cast<float *>(packed);
-        if (hipMemsetAsync(hdr + mlpk::HDR_ESCALE, 0, sizeof(float) * (2 + L.n_l512), st) != hipSuccess)
+        if (hipMemsetAsync(hdr + mlpk::HDR_ESCALE, 0, sizeof(float) * (1 + L.n_l512), st) != hipSuccess)
             return fail(PNR_ERR_HIP, "mlp_pack: hipMemsetAsync failed");
-        hipLaunchKernelGGL(mlpk::k_layer_absmax, dim3(32, (unsigned)(2 + L.n_l512)), dim3(256), 0, st, s, L, hdr);
+        hipLaunchKernelGGL(mlpk::k_layer_absmax, dim3(32, (unsigned)(1 + L.n_l512)), dim3(256), 0, st, s, L, hdr);
         if (!launch_ok("mlp_layer_absmax")) return PNR_ERR_HIP;
-        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3(1), dim3(64), 0, st, 2 + L.n_l512, hdr);
+        hipLaunchKernelGGL(mlpk::k_layer_escale, dim3(1), dim3(64), 0, st, 1 + L.n_l512, hdr);
         if (!launch_ok("mlp_layer_escale")) return PNR_ERR_HIP;
-        hipLaunchKernelGGL(mlpk::k_pack_f16, dim3((unsigned)((n + mlpk::KS32 * 64 + 255) / 256)), dim3(256), 0, st,
+        hipLaunchKernelGGL(mlpk::k_pack_f16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
                            s, L, static_cast<float *>(packed));
         if (!launch_ok("mlp_pack_f16")) return PNR_ERR_HIP;
     } else if (L.prec) {

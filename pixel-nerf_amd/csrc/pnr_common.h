@@ -107,6 +107,15 @@ __device__ __forceinline__ float rows_max(float m) {
     return max_nc(__uint_as_float(r32[0]), __uint_as_float(r32[1]));
 }
 
+// sum over the four 16-lane rows of a wave (v_permlane16/32_swap; every lane gets the same
+// ((r0 + r1) + (r2 + r3)) in some operand order: IEEE addition is commutative, so the lanes agree)
+__device__ __forceinline__ float rows_sum(float m) {
+    const auto r16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    m = __uint_as_float(r16[0]) + __uint_as_float(r16[1]);
+    const auto r32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    return __uint_as_float(r32[0]) + __uint_as_float(r32[1]);
+}
+
 // ---- counter-based random streams (pnr_rng {seed, offset}, include/pnr_abi.h) ----------
 // Philox4x32-10 (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1, 2, 3",
 // SC'11; the Random123 constants).  Draw e of stream s keyed by `seed` uses the counter
