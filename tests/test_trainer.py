@@ -188,3 +188,119 @@ def test_train_script_end_to_end_and_resume(tmp_path):
     assert r2.returncode == 0, r2.stderr[-3000:]
     assert "Load" in r2.stdout
     assert torch.load(str(ck / "_iter"), weights_only=True)["iter"] == 5
+
+
+# ---- Trainer over 2 gloo ranks (CPU): sampler sharding, gradient mean, rank-0 checkpoints --------
+class _TinyNet(torch.nn.Module):
+    """PixelNeRFNet stand-in: encode() keeps the mean source colour; the "render" is
+    sigmoid(w * (o + d)) + that colour; an encoder BatchNorm for the SyncBN switch."""
+
+    def __init__(self):
+        super().__init__()
+        self.encoder = torch.nn.Sequential(torch.nn.BatchNorm2d(3))
+        self.w = torch.nn.Parameter(torch.full((3,), 0.5))
+        self.col = None
+
+    def encode(self, images, poses, focal, c=None):
+        self.col = images.mean(dim=(0, 1, 3, 4))
+
+    def load_weights(self, args, opt_init=False, strict=True, device=None):
+        path = os.path.join(args.checkpoints_path, args.name, "pixel_nerf_latest")
+        if args.resume and os.path.exists(path):
+            self.load_state_dict(torch.load(path, weights_only=True))
+        return self
+
+    def save_weights(self, args, opt_init=False):
+        torch.save(self.state_dict(), os.path.join(args.checkpoints_path, args.name, "pixel_nerf_latest"))
+
+
+class _TinyRenderer(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("iter_idx", torch.zeros((), dtype=torch.long))
+
+    def bind_parallel(self, net, gpus=None, simple_output=False):
+        def render(rays, want_weights=False):
+            return {"coarse": {"rgb": torch.sigmoid(net.w * (rays[..., :3] + rays[..., 3:6])) + 0.1 * net.col}}
+        return render
+
+    def sched_step(self, steps=1):
+        self.iter_idx += steps
+
+
+class _Objects(torch.utils.data.Dataset):
+    z_near, z_far, lindisp = 0.5, 2.5, False
+
+    def __init__(self, n=8, nv=3, size=6):
+        g = torch.Generator().manual_seed(1)
+        self.items = []
+        for i in range(n):
+            poses = torch.eye(4).repeat(nv, 1, 1)
+            poses[:, :3, 3] = torch.rand(nv, 3, generator=g)
+            self.items.append(dict(images=torch.rand(nv, 3, size, size, generator=g) * 2 - 1, poses=poses,
+                                   focal=torch.tensor(5.0 + i), c=torch.tensor([3.0, 3.0]),
+                                   bbox=torch.tensor([[1.0, 1.0, 4.0, 4.0]]).repeat(nv, 1), obj=torch.tensor(i)))
+
+    def __len__(self):
+        return len(self.items)
+
+    def __getitem__(self, i):
+        return self.items[i]
+
+
+def _trainer_args(ck, resume=False):
+    import types
+
+    return types.SimpleNamespace(checkpoints_path=ck, name="tiny", resume=resume, batch_size=2, lr=0.05,
+                                 gamma=1.0, gamma_delay=0, epochs=1, ray_batch_size=16, nviews=[1],
+                                 no_bbox_step=100)
+
+
+def _trainer_worker(rank, world, port, ck, q):
+    from pnr import dist as pdist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    pdist.init_from_env("gloo")
+    trainer.seed_everything(rank)
+    net = _TinyNet()
+    t = trainer.Trainer(net, _TinyRenderer(), _Objects(), None, _trainer_args(ck), {"print_interval": 100,
+                        "save_interval": 100}, torch.device("cpu"), log=lambda *_: None)
+    seen = [int(o) for d in t.loader for o in d["obj"]]
+    last = t.start()
+    # plain Python values: a tensor put on the queue is shared through a handle that dies with
+    # this process
+    q.put((rank, seen, net.w.detach().tolist(), type(net.encoder[0]).__name__, dict(last)))
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_trainer_two_rank_gloo(tmp_path):
+    """pnr.trainer.Trainer at world_size 2 (gloo): each rank draws its own objects (together all
+    of them, once), the gradient mean keeps the two ranks' parameters identical through Adam, the
+    encoder BatchNorm became SyncBatchNorm2d, and only rank 0 wrote the checkpoints (_iter = the
+    steps of one rank: 4 objects / 2 per batch)."""
+    import multiprocessing
+
+    from test_dist import _free_port
+
+    ctx = multiprocessing.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ck = str(tmp_path / "ck")
+    procs = [ctx.Process(target=_trainer_worker, args=(r, 2, port, ck, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, seen0, w0, bn0, l0), (r1, seen1, w1, bn1, l1) = res
+    assert sorted(seen0 + seen1) == list(range(8)) and not set(seen0) & set(seen1)
+    w0, w1 = torch.tensor(w0), torch.tensor(w1)
+    assert torch.equal(w0, w1) and not torch.equal(w0, torch.full((3,), 0.5))
+    assert bn0 == bn1 == "SyncBatchNorm2d"
+    assert np.isfinite(l0["t"]) and np.isfinite(l1["t"])
+    assert torch.load(os.path.join(ck, "tiny", "_iter"), weights_only=True)["iter"] == 2
+    assert torch.equal(torch.load(os.path.join(ck, "tiny", "pixel_nerf_latest"), weights_only=True)["w"], w0)
