@@ -19,6 +19,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from .consts import device_const
+from .prof import ranged
 
 __all__ = ["SpatialEncoder", "ImageEncoder", "resnet34_trunk"]
 
@@ -388,6 +389,7 @@ class SpatialEncoder(nn.Module):
         through each map's upsample adjoint (``LatentChannelsLast``)."""
         return self.set_latent_cl(LatentChannelsLast.apply(*maps))
 
+    @ranged("encoder_index")
     def index(self, uv, cam_z=None, image_size=(), z_bounds=None):
         """Bilinear feature lookup at image points (encoder.py:80-109); utility only —
         the ray march does this gather inside the fused HIP kernel."""

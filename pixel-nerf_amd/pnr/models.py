@@ -28,6 +28,7 @@ from . import _lib
 from .consts import device_const
 from .conf import as_conf
 from .encoder import ImageEncoder, SpatialEncoder
+from .prof import ranged
 from .util import combine_interleaved, repeat_interleave
 
 __all__ = ["PositionalEncoding", "ResnetBlockFC", "ResnetFC", "PixelNeRFNet", "make_model",
@@ -86,6 +87,7 @@ class PositionalEncoding(nn.Module):
         phases[1::2] = np.pi * 0.5
         self.register_buffer("_phases", phases.view(1, -1, 1))
 
+    @ranged("positional_enc")
     def forward(self, x):
         embed = x.unsqueeze(1).repeat(1, self.num_freqs * 2, 1)
         embed = torch.sin(torch.addcmul(self._phases, embed, self._freqs))
@@ -119,6 +121,7 @@ class ResnetBlockFC(nn.Module):
         if size_in != size_out:
             self.shortcut = nn.Linear(size_in, size_out, bias=False)
 
+    @ranged("resblock")
     def forward(self, x):
         h = self.fc_0(self.activation(x))
         res = x if self.shortcut is None else self.shortcut(x)
@@ -154,6 +157,7 @@ class ResnetFC(nn.Module):
             if use_spade:
                 self.scale_z = nn.ModuleList([nn.Linear(d_latent, d_hidden) for _ in range(n_lin_z)])
 
+    @ranged("resnetfc_infer")
     def forward(self, zx, combine_inner_dims=(1,), combine_index=None, dim_size=None):
         """(N, d_latent + d_in) -> (N', d_out) (resnetfc.py:132-184), as device torch ops: the
         callback path of PixelNeRFNet confs the fused kernel does not implement (the fused
@@ -554,6 +558,7 @@ class PixelNeRFNet(nn.Module):
                 mlp.drop_latent_proj()
 
     # ---- forward (point query) -----------------------------------------------------
+    @ranged("model_inference")
     def forward(self, xyz, coarse=True, viewdirs=None, far=False):
         """(SB, B, 3) world points -> (SB, B, 4) [sigmoid(rgb), relu(sigma)]
         (models.py:146-266) on the HIP device: the fused kernel for the confs it implements,

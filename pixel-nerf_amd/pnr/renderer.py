@@ -23,6 +23,7 @@ model-callback and training paths always draw with torch in the reference's orde
 import torch
 
 from . import _lib, ops
+from .prof import ranged
 from .conf import as_conf
 
 __all__ = ["NeRFRenderer", "DotMap"]
@@ -131,6 +132,7 @@ class NeRFRenderer(torch.nn.Module):
             u = torch.rand(rays.shape[0], self.n_coarse, device=rays.device)
         return ops.sample_coarse(rays, self.n_coarse, u, self.lindisp)
 
+    @ranged("renderer_composite")
     def composite(self, model, rays, z_samp, coarse=True, sb=0):
         """nerf.py:163-249 through the model callback; compositing on the HIP kernel."""
         B, K = z_samp.shape
@@ -164,6 +166,7 @@ class NeRFRenderer(torch.nn.Module):
         return ops.composite(z_samp, raw, rays, self.white_bkgd)
 
     # ---- forward (nerf.py:251-303) ---------------------------------------------------
+    @ranged("renderer_forward")
     def forward(self, model, rays, want_weights=False):
         if self.sched is not None and self.last_sched.item() > 0:
             self.n_coarse = self.sched[1][self.last_sched.item() - 1]
