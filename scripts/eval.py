@@ -18,6 +18,7 @@ import argparse
 import os
 import sys
 import time
+import traceback
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "pixel-nerf_amd"))
@@ -94,45 +95,50 @@ def main(argv=None):
     os.makedirs(args.output, exist_ok=True)
     finish = open(os.path.join(args.output, "finish.txt"), "a", buffering=1)
     for obj_idx in range(len(dset)):
-        data = dset[obj_idx]
-        name = os.path.basename(data["path"])
-        out_dir = os.path.join(args.output, name)
-        os.makedirs(out_dir, exist_ok=True)
-        images, poses = data["images"], data["poses"]
-        if images.shape[0] < 2:
-            print("Skipping %s - less than 2 views" % name, flush=True)
-            continue
-        focal = torch.as_tensor(data["focal"], dtype=torch.float32)[None].to(device)
-        c = data.get("c")
-        c = c.to(device).unsqueeze(0) if c is not None else None
-        src = torch.zeros(images.shape[0], dtype=torch.bool)
-        src[source] = True
-        with torch.no_grad():
-            net.encode(images[src].to(device).unsqueeze(0), poses[src].to(device).unsqueeze(0), focal, c=c)
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        sig = density_grid(net, args.mesh_res, device)
-        torch.cuda.synchronize(device)
-        dt = time.perf_counter() - t0
-        sig_np = sig.cpu().numpy()
-        np.save(os.path.join(out_dir, name + "_sigma.npy"), sig_np)
-        meshed = export_mesh(sig_np, args.mesh_thresh, os.path.join(out_dir, name + "_mesh.stl"))
-        print("%s: density grid %d^3 in %.3f s (%.1f M points/s)%s" % (
-            name, args.mesh_res, dt, args.mesh_res ** 3 / dt / 1e6,
-            "" if meshed else "; mesh export skipped (skimage / trimesh not installed)"), flush=True)
-        if not args.compare:
-            continue
-        tgt = ~src
-        H, W = images.shape[-2:]
-        rays = util.gen_rays(poses[tgt].to(device), W, H, focal, dset.z_near, dset.z_far, c=c).reshape(-1, 8)
-        with torch.no_grad():
-            rgb = torch.cat([render_par(r[None])[0][0] for r in torch.split(rays, args.ray_batch_size, dim=0)])
-        rgb = rgb.clamp(0.0, 1.0).reshape(-1, H, W, 3).cpu().numpy()
-        gt = (images[tgt] * 0.5 + 0.5).permute(0, 2, 3, 1).numpy()
-        psnr = float(np.mean([evaluate.psnr_np(rgb[i], gt[i]) for i in range(len(gt))]))
-        ssim = float(np.mean([evaluate.ssim(rgb[i], gt[i]) for i in range(len(gt))]))
-        print("PSNR: %.2f, SSIM: %.4f" % (psnr, ssim), flush=True)
-        finish.write("%s %.2f %.4f 1\n" % (name, psnr, ssim))
+        name = str(obj_idx)
+        try:
+            data = dset[obj_idx]
+            name = os.path.basename(data["path"])
+            out_dir = os.path.join(args.output, name)
+            os.makedirs(out_dir, exist_ok=True)
+            images, poses = data["images"], data["poses"]
+            if images.shape[0] < 2:
+                print("Skipping %s - less than 2 views" % name, flush=True)
+                continue
+            focal = torch.as_tensor(data["focal"], dtype=torch.float32)[None].to(device)
+            c = data.get("c")
+            c = c.to(device).unsqueeze(0) if c is not None else None
+            src = torch.zeros(images.shape[0], dtype=torch.bool)
+            src[source] = True
+            with torch.no_grad():
+                net.encode(images[src].to(device).unsqueeze(0), poses[src].to(device).unsqueeze(0), focal, c=c)
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            sig = density_grid(net, args.mesh_res, device)
+            torch.cuda.synchronize(device)
+            dt = time.perf_counter() - t0
+            sig_np = sig.cpu().numpy()
+            np.save(os.path.join(out_dir, name + "_sigma.npy"), sig_np)
+            meshed = export_mesh(sig_np, args.mesh_thresh, os.path.join(out_dir, name + "_mesh.stl"))
+            print("%s: density grid %d^3 in %.3f s (%.1f M points/s)%s" % (
+                name, args.mesh_res, dt, args.mesh_res ** 3 / dt / 1e6,
+                "" if meshed else "; mesh export skipped (skimage / trimesh not installed)"), flush=True)
+            if not args.compare:
+                continue
+            tgt = ~src
+            H, W = images.shape[-2:]
+            rays = util.gen_rays(poses[tgt].to(device), W, H, focal, dset.z_near, dset.z_far, c=c).reshape(-1, 8)
+            with torch.no_grad():
+                rgb = torch.cat([render_par(r[None])[0][0] for r in torch.split(rays, args.ray_batch_size, dim=0)])
+            rgb = rgb.clamp(0.0, 1.0).reshape(-1, H, W, 3).cpu().numpy()
+            gt = (images[tgt] * 0.5 + 0.5).permute(0, 2, 3, 1).numpy()
+            psnr = float(np.mean([evaluate.psnr_np(rgb[i], gt[i]) for i in range(len(gt))]))
+            ssim = float(np.mean([evaluate.ssim(rgb[i], gt[i]) for i in range(len(gt))]))
+            print("PSNR: %.2f, SSIM: %.4f" % (psnr, ssim), flush=True)
+            finish.write("%s %.2f %.4f 1\n" % (name, psnr, ssim))
+        except Exception as e:   # eval.py:146-149: report the object and go on
+            print("ERROR processing %s: %s" % (name, e), flush=True)
+            traceback.print_exc()
     finish.close()
 
 
