@@ -304,3 +304,35 @@ def test_trainer_two_rank_gloo(tmp_path):
     assert np.isfinite(l0["t"]) and np.isfinite(l1["t"])
     assert torch.load(os.path.join(ck, "tiny", "_iter"), weights_only=True)["iter"] == 2
     assert torch.equal(torch.load(os.path.join(ck, "tiny", "pixel_nerf_latest"), weights_only=True)["w"], w0)
+
+
+@pytest.mark.gpu
+def test_train_script_two_ranks(tmp_path):
+    """scripts/train.py under torch.distributed.run with 2 ranks (both on device 0 over gloo: the
+    one-GPU box cannot run RCCL with two ranks on one card; a node puts one rank per GPU over
+    RCCL): each rank trains its own objects with the encoder BatchNorm synchronised and the
+    gradient mean over the ranks; rank 0 writes the checkpoints."""
+    import socket
+
+    inp = make_inputs(n_obj=4, n_views=3, size=24, seed=6)
+    root = write_srn_dir(str(tmp_path), inp, stage="train")
+    write_srn_dir(str(tmp_path), make_inputs(n_obj=2, n_views=3, size=24, seed=7), stage="val")
+    write_srn_dir(str(tmp_path), make_inputs(n_obj=1, n_views=3, size=24, seed=8), stage="test")
+    (tmp_path / "train.conf").write_text(TRAIN_CONF)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PNR_DIST_BACKEND="gloo", PNR_FORCE_DEVICE="0", OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "scripts", "train.py"),
+           "-c", str(tmp_path / "train.conf"), "-D", root, "-n", "synth2", "--checkpoints_path", str(tmp_path / "ck"),
+           "-B", "1", "-V", "1", "-R", "32", "--image_size", "24", "--max_steps", "2"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert r.stdout.count("final losses") == 1, r.stdout[-2000:]
+    ck = tmp_path / "ck" / "synth2"
+    assert torch.load(str(ck / "_iter"), weights_only=True)["iter"] == 2
+    sd = torch.load(str(ck / "pixel_nerf_latest"), weights_only=True)
+    assert all(bool(torch.isfinite(v).all()) for v in sd.values() if v.is_floating_point())
