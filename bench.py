@@ -106,6 +106,16 @@ RAY_BATCH = 50000              # gen_video.py --ray_batch_size default (args.py:
 CHUNK = 4096
 W = H = 128
 FUSED_MARCH = True   # pnr_render_set_fused(2) (main: --unfused / --fused-mode)
+# why the single-launch march (mode 3, north_star's "one fused kernel") is selectable but not the
+# default (measured in round 4)
+MARCH_MODE_BOUND = {
+    "default_mode": 2, "single_launch_mode": 3,
+    "mode3_upside_bound_pct": 0.15,
+    "why": "mode 3 can only save what mode 2 spends outside its two k_point_mlp launches: the k_sample_fine "
+           "launch (0.06 ms per 50,000-ray chunk) and one launch tail (~0.1 ms), ~0.15 % of a ~106 ms chunk; "
+           "it pays the fine draws on one wave while seven wait (~0.6 % of tile work) and measured 0.8 % "
+           "slower. Mode 3 is bit-identical to modes 0-2 (tests/test_gpu_parity.py::"
+           "test_fused_march_matches_unfused) and runs with --fused-mode 3."}
 MARCH_MODE = 2       # the fused mode (3: both passes in one launch)
 KERNELS = ["sample_coarse", "mlp_coarse", "composite_coarse", "sample_fine", "mlp_fine", "composite_fine"]
 
@@ -208,18 +218,97 @@ class RenderProbe:
         }
 
 
-def timed(fn, steps, warmup, dev, world):
+class ClockSampler:
+    """The GPU's graphics clock sampled from the SMI library (amdsmi) in a background thread while
+    `on` -- the sustained clock of the timed region, recorded in the line so a reader can place
+    a run within the box-to-box spread (MI355X_MICROARCH.md "DVFS give-back": the SMI clock reads up
+    to ~10 % above the in-kernel clock; profiles/<run>/clock.csv holds the GRBM_GUI_ACTIVE-derived
+    one of the same lease).  The device is matched by PCI bus id; any failure leaves it off."""
+
+    def __init__(self, dev, period_s=0.05):
+        self.samples, self.err, self.h, self.period = [], None, None, period_s
+        self._stop = None
+        try:
+            import amdsmi
+
+            self.smi = amdsmi
+            amdsmi.amdsmi_init()
+            props = torch.cuda.get_device_properties(dev)
+            bus = getattr(props, "pci_bus_id", None)
+            for h in amdsmi.amdsmi_get_processor_handles():
+                bdf = str(amdsmi.amdsmi_get_gpu_device_bdf(h))    # "0000:75:00.0"
+                if bus is None or int(bdf.split(":")[1], 16) == int(bus):
+                    self.h = h
+                    self.bdf = bdf
+                    break
+            if self.h is None:
+                self.err = "no SMI handle with PCI bus %s" % bus
+        except Exception as e:   # noqa: BLE001 -- the clock is an annotation, never a failure
+            self.err = "%s: %s" % (type(e).__name__, e)
+
+    def _read(self):
+        m = self.smi.amdsmi_get_gpu_metrics_info(self.h)
+        xs = [v for v in (m.get("current_gfxclks") or []) if isinstance(v, (int, float)) and 0 < v < 10000]
+        if xs:
+            return sum(xs) / len(xs)
+        v = m.get("current_gfxclk")
+        if isinstance(v, (int, float)) and 0 < v < 10000:
+            return float(v)
+        return float(self.smi.amdsmi_get_clock_info(self.h, self.smi.AmdSmiClkType.GFX)["clk"])
+
+    def start(self):
+        import threading
+
+        if self.h is None:
+            return
+        self.samples = []
+        self._stop = threading.Event()
+
+        def loop():
+            while not self._stop.is_set():
+                try:
+                    self.samples.append(self._read())
+                except Exception as e:   # noqa: BLE001
+                    self.err = "%s: %s" % (type(e).__name__, e)
+                    return
+                self._stop.wait(self.period)
+
+        self._t = threading.Thread(target=loop, daemon=True)
+        self._t.start()
+
+    def stop(self):
+        if self._stop is None:
+            return
+        self._stop.set()
+        self._t.join()
+        self._stop = None
+
+    def summary(self):
+        if not self.samples:
+            return {"mhz_mean": None, "error": self.err or "no samples"}
+        s = sorted(self.samples)
+        return {"mhz_mean": round(sum(s) / len(s), 1), "mhz_median": s[len(s) // 2], "mhz_min": s[0],
+                "mhz_max": s[-1], "samples": len(s), "device_bdf": getattr(self, "bdf", None),
+                "source": "amdsmi gpu_metrics current_gfxclk(s), sampled every %d ms over the timed region"
+                          % int(self.period * 1000)}
+
+
+def timed(fn, steps, warmup, dev, world, clock=None):
     """W untimed steps, then K timed steps between barrier + synchronize; max over ranks."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    if clock is not None:
+        clock.start()
     t0 = time.perf_counter()
     for _ in range(steps):
         res = fn()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    if clock is not None:
+        clock.stop()
     if world > 1:
         dist.barrier()
     return pdist.max_over_ranks(t1 - t0, device=dev), res
@@ -246,7 +335,7 @@ def make_net(dev, precision, latent_proj, use_first_pool=True):
     return net
 
 
-def cfg3_leg(args, dev, rank, world, probe):
+def cfg3_leg(args, dev, rank, world, probe, clock=None):
     net = make_net(dev, args.precision, not args.no_latent_proj, use_first_pool=False)
     # the eval encode runs the BN-folded trunk replayed as one HIP graph (pnr.encoder.InferenceTrunk);
     # --encoder-eager: the module's own conv / BN / relu launches (A/B)
@@ -276,7 +365,7 @@ def cfg3_leg(args, dev, rank, world, probe):
             step()
         probe.reset()
         probe.on = True
-        elapsed, rgb = timed(step, args.steps, 0, dev, world)
+        elapsed, rgb = timed(step, args.steps, 0, dev, world, clock=clock)
         probe.on = False
     assert bool(torch.isfinite(rgb).all())
     avg, roof = probe.summary(args.precision, net.use_latent_proj)
@@ -482,8 +571,12 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
 
 
 # ----------------------------------------------------------------- roofline helpers --
-def composite_roofline(dev, ev):
-    """Standalone composite kernel on 1 M rays x 128 samples (HBM-bound)."""
+def composite_roofline(dev, ev, pmc_path=None, same_lease=False):
+    """Standalone composite kernel on 1 M rays x 128 samples (HBM-bound): algorithmic bytes
+     / HIP-event time, and -- when a PMC summary holds this leg's launches
+    (workload composite_1M, scripts/summarize_profile.py) -- the counter bytes per launch and
+    counter GB/s (counter bytes / the same HIP-event time) beside them (north_star: "rocprof HBM
+    GB/s on the composite step")."""
     from pnr import ops
 
     B, K = 1 << 20, 128
@@ -515,9 +608,21 @@ def composite_roofline(dev, ev):
         ms = sorted(times)[len(times) // 2]
         per_ray = 4 * K + 16 * K + 4 + 12 + 4 + (4 * K if want_w else 0)
         gbs = per_ray * B / (ms * 1e-3) / 1e9
-        res["weights" if want_w else "no_weights"] = dict(
+        key = "weights" if want_w else "no_weights"
+        res[key] = dict(
             ms=round(ms, 4), bytes_per_ray=per_ray, achieved=round(gbs, 1), peak=HBM_PEAK_GBS,
             unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4))
+        if pmc_path and os.path.exists(pmc_path):
+            rows = [(b, dms) for k, g, dms, b, p, w in pmc_rows(pmc_path)
+                    if "k_composite" in k and w == "composite_1M" and p == key]
+            if rows:
+                tb = sum(b for b, _ in rows) / len(rows)
+                res[key]["pmc"] = dict(
+                    hbm_bytes_per_launch=int(tb), algorithmic_bytes_per_launch=per_ray * B,
+                    traffic_over_algorithmic=round(tb / (per_ray * B), 4),
+                    counter_gbs=round(tb / (ms * 1e-3) / 1e9, 1),
+                    counter_frac=round(tb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    launches=len(rows), source=pmc_source_label(pmc_path, same_lease))
     return res
 
 
@@ -681,23 +786,46 @@ def l2_stream(points, launch_ms, precision, latent_proj):
             "frac_of_gather_loop": round(tbs / L2_GATHER_LOOP_TBS, 4)}
 
 
-def pmc_traffic(kernel, render_pass, workload):
-    """Mean HBM bytes per launch of `kernel` in `render_pass` of `workload` from the newest
-    committed PMC summary that has it (rocprofv3 counters cannot be read live from inside
-    the process).  Returns (bytes, summary path) or (None, None)."""
+def pmc_rows(path):
+    """Rows of a pmc_summary.csv (scripts/summarize_profile.py): (kernel, grid, dispatch_ms,
+    hbm_bytes_corrected, pass, workload)."""
     import csv
+
+    with open(path) as fh:
+        rows = list(csv.reader(ln for ln in fh if not ln.startswith("#") and not ln.startswith("kernel,")))
+    return [(f[0], int(f[1]), float(f[2]), int(f[5]), f[6], f[7]) for f in rows if f and len(f) > 7]
+
+
+def pmc_summary_path(explicit=None):
+    """The PMC summary the line's `traffic` figures come from: --traffic-from (a summary written
+    by the same GPU lease, scripts/gpu_session.sh `evidence`), else the newest committed
+    profiles/*/pmc_summary.csv.  Returns (path, same_lease)."""
     import glob
 
-    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")), reverse=True):
-        vals = []
-        with open(path) as fh:
-            rows = list(csv.reader(ln for ln in fh if not ln.startswith("#") and not ln.startswith("kernel,")))
-        for f in rows:   # kernel names are quoted (they contain commas: k_point_mlp<3, true>)
-            if f and f[0].endswith(kernel) and len(f) > 7 and f[6] == render_pass and f[7] == workload:
-                vals.append(int(f[5]))
-        if vals:
-            return sum(vals) // len(vals), os.path.relpath(path, REPO)
-    return None, None
+    if explicit:
+        return explicit, True
+    paths = sorted(glob.glob(os.path.join(REPO, "profiles", "*", "pmc_summary.csv")), reverse=True)
+    return (paths[0], False) if paths else (None, False)
+
+
+def pmc_traffic(kernel, render_pass, workload, path):
+    """Mean HBM bytes per launch of `kernel` in `render_pass` of `workload` in the PMC summary at
+    `path` (rocprofv3 counters cannot be read live from inside the process).  Returns bytes or None."""
+    if not path or not os.path.exists(path):
+        return None
+    vals = [b for k, _, _, b, p, w in pmc_rows(path) if k.endswith(kernel) and p == render_pass and w == workload]
+    return sum(vals) // len(vals) if vals else None
+
+
+def pmc_source_label(path, same_lease):
+    if path is None:
+        return None
+    rel = os.path.relpath(path, REPO)
+    if same_lease:
+        return ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes run in the same GPU lease as this bench, just "
+                "before it (%s; FETCH x2 gfx950 correction)" % rel)
+    return ("committed PMC summary %s from an EARLIER lease, not measured in this run (FETCH x2 gfx950 "
+            "correction)" % rel)
 
 
 # ----------------------------------------------------------------- CPU baseline -----
@@ -902,6 +1030,10 @@ def main():
                     help="per-point lin_z GEMMs on the gathered latent (A/B against the projection)")
     ap.add_argument("--unfused", action="store_true",
                     help="separate sample / MLP / composite kernels instead of the fused ray march (A/B)")
+    ap.add_argument("--traffic-from", default=None,
+                    help="pmc_summary.csv written by this GPU lease (scripts/gpu_session.sh evidence); default: "
+                         "the newest committed profiles/*/pmc_summary.csv, labelled as such")
+    ap.add_argument("--no-clock", action="store_true", help="do not sample the GPU clock (amdsmi)")
     ap.add_argument("--fused-mode", type=int, default=2,
                     help="pnr_render_set_fused: 2 fused passes + fine-draw kernel (default), 1 fine draws "
                          "in the coarse epilogue too, 3 both passes in one launch")
@@ -923,12 +1055,12 @@ def main():
     ev = HipEvents()
     probe = RenderProbe(ev)
 
-    net3, nmr, elapsed, avg, roof, enc_ms, (start, end) = cfg3_leg(args, dev, rank, world, probe)
+    clock = None if args.no_clock else ClockSampler(dev)
+    net3, nmr, elapsed, avg, roof, enc_ms, (start, end) = cfg3_leg(args, dev, rank, world, probe, clock)
     n_batch = nmr[3].shape[0]
-    traffic, traffic_src = pmc_traffic(roof["kernel_name"], "fine", "cfg3")
-    roof["traffic"] = traffic
-    roof["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, fine-pass "
-                              "launches of %s (%s, FETCH x2 gfx950 correction)" % (roof["kernel_name"], traffic_src))
+    pmc_path, same_lease = pmc_summary_path(args.traffic_from)
+    roof["traffic"] = pmc_traffic(roof["kernel_name"], "fine", "cfg3", pmc_path)
+    roof["traffic_source"] = pmc_source_label(pmc_path, same_lease)
     out = {
         "metric": "rays/sec (coarse+fine, 64+64 samples)",
         "value": round(n_batch * args.steps / elapsed, 1),
@@ -962,6 +1094,8 @@ def main():
                    "per_step": "encode (ResNet34) + latent projection + render + device->host copy"},
         "encode_ms": round(enc_ms, 3),
         "roofline": roof,
+        "box_clock": clock.summary() if clock is not None else None,
+        "march_mode_bound": MARCH_MODE_BOUND,
         "kernel_ms": {k: round(v, 4) for k, v in avg.items()},
         "l2_stream": l2_stream(roof["points_per_launch"], roof["launch_ms"], args.precision,
                                not args.no_latent_proj),
@@ -972,7 +1106,7 @@ def main():
         if not args.no_cfg2:
             out["cfg2"] = cfg2_leg(args, dev, probe)
         if not args.no_composite:
-            out["composite"] = composite_roofline(dev, ev)
+            out["composite"] = composite_roofline(dev, ev, pmc_path, same_lease)
         if not args.no_extra:
             out["extra_configs"] = extra_configs(dev, args.precision, not args.no_latent_proj, probe,
                                                  0 if args.no_cpu else 64)
