@@ -1,2 +1,5 @@
-"""Compat shim: ``from model import make_model`` (reference src/model/__init__.py)."""
+"""Compat shim: ``from model import make_model`` / ``from model import loss`` (reference
+src/model/__init__.py, src/model/loss.py)."""
 from pnr.models import PixelNeRFNet, make_model  # noqa: F401
+
+from . import loss  # noqa: F401,E402

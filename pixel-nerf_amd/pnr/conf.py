@@ -21,6 +21,8 @@ class Conf(dict):
     """dict with pyhocon-style typed getters; nested dicts come back as Conf."""
 
     def __getitem__(self, k):
+        if not dict.__contains__(self, k) and isinstance(k, str) and "." in k:
+            return self._get(k)   # conf["loss.rgb"] reaches into subtrees, as pyhocon does (train.py:111)
         v = dict.__getitem__(self, k)
         return Conf(v) if isinstance(v, dict) and not isinstance(v, Conf) else v
 

@@ -517,10 +517,6 @@ class PixelNeRFNet(nn.Module):
         r = self.hip_unsupported_reason()
         if r:
             raise NotImplementedError("pnr: " + r)
-        if torch.is_grad_enabled() and self.needs_grad():
-            raise NotImplementedError(
-                "pnr: point queries are forward-only; training runs through "
-                "NeRFRenderer.forward (pnr/train.py). Use torch.no_grad() for queries")
 
     def hip_scene(self):
         lat = self.encoder.latent_cl
@@ -562,13 +558,24 @@ class PixelNeRFNet(nn.Module):
     def forward(self, xyz, coarse=True, viewdirs=None, far=False):
         """(SB, B, 3) world points -> (SB, B, 4) [sigmoid(rgb), relu(sigma)]
         (models.py:146-266) on the HIP device: the fused kernel for the confs it implements,
-        device torch ops (the callback path) for the others."""
+        device torch ops (the callback path) for the others.
+
+        With grad enabled and trainable parameters (or a latent that carries gradient) the output
+        carries the reference's autograd graph, as the reference's does: eval/eval.py:100 and
+        train/train.py:422 query without torch.no_grad().  The query then runs the training
+        forward (``train.RenderPoints`` on rays o = xyz, d = viewdirs at z = 0, so o + z d = xyz
+        exactly), differentiable in the MLP parameters and the latent; a query whose xyz or
+        viewdirs themselves require grad takes the device torch ops (differentiable in them too)."""
         if self.fused_conf_reason() is not None:
             return self._forward_torch(xyz, coarse, viewdirs)
         self._require_hip()
         SB, B, _ = xyz.shape
         if SB != self.num_objs:
             raise ValueError("xyz has %d objects but encode() saw %d" % (SB, self.num_objs))
+        if torch.is_grad_enabled() and self.needs_grad():
+            if xyz.requires_grad or (viewdirs is not None and viewdirs.requires_grad):
+                return self._forward_torch(xyz, coarse, viewdirs)
+            return self._forward_points_grad(xyz, coarse, viewdirs)
         from .ops import _dev
 
         from . import torchops
@@ -579,6 +586,25 @@ class PixelNeRFNet(nn.Module):
         proj = self.hip_proj(coarse)
         return torchops.load().point_query(*torchops.scene_args(self), torchops.desc_list(desc), packed, proj,
                                            xyz, vd)
+
+    def _forward_points_grad(self, xyz, coarse, viewdirs):
+        """The point query with its autograd graph (see forward): one training-forward sample per
+        point, rays [xyz, viewdirs, 0, 0] at z = 0."""
+        from .ops import _dev
+        from .train import RenderPoints, mlp_params
+
+        SB, B, _ = xyz.shape
+        xyz = _dev(xyz, "xyz").detach().float()
+        vd = (_dev(viewdirs, "viewdirs").detach().float().reshape(SB, B, 3) if viewdirs is not None
+              else torch.zeros_like(xyz))
+        rays = torch.cat((xyz, vd, torch.zeros(SB, B, 2, device=xyz.device)), -1).reshape(SB * B, 8).contiguous()
+        z = torch.zeros(SB * B, 1, device=xyz.device)
+        lat = self.encoder.latent_cl
+        if self.stop_encoder_grad:
+            lat = lat.detach()
+        mlp = self.mlp_coarse if (coarse or self.mlp_fine is None) else self.mlp_fine
+        raw = RenderPoints.apply(self, coarse, rays, z, lat, *mlp_params(mlp))
+        return raw.reshape(SB, B, 4)
 
     def _forward_torch(self, xyz, coarse, viewdirs):
         """models.py:146-266 as device torch ops (hipBLASLt GEMMs, grid_sample): the callback

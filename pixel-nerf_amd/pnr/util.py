@@ -10,6 +10,14 @@ These mirror the semantics (not the code) of the reference's ``src/util/util.py`
 * ``psnr``                — util.py:474-481
 * ``bbox_sample``         — util.py:220-235 (the training step's pixel picks inside object boxes)
 
+and the rest of what the reference's callers reach through ``util.X`` (eval/gen_video.py,
+eval/eval_approx.py, eval/eval.py, eval/eval_real.py, train/train.py; tests/test_dropin.py scans
+them): ``get_cuda`` (util.py:193-202), ``cmap`` / ``image_float_to_uint8`` (util.py:13-30),
+``quat_to_rot`` / ``rot_to_quat`` (util.py:484-528), ``coord_from_blender`` / ``coord_to_blender``
+(util.py:146-171), ``look_at`` (util.py:174-190), ``get_image_to_tensor_balanced`` /
+``get_mask_to_tensor`` (util.py:68-81), ``masked_sample`` (util.py:205-217), ``homogeneous``,
+``gen_grid``, ``batched_index_select_nd_last``, ``count_parameters``, ``get_module``.
+
 They run on whatever device their inputs live on; none of them is on the
 per-point hot path (ray generation on device is SURVEY §8(f) rank 1).
 """
@@ -26,7 +34,26 @@ __all__ = [
     "pose_spherical",
     "psnr",
     "batched_index_select_nd",
+    "batched_index_select_nd_last",
     "bbox_sample",
+    "masked_sample",
+    "get_cuda",
+    "image_float_to_uint8",
+    "cmap",
+    "quat_to_rot",
+    "rot_to_quat",
+    "coord_from_blender",
+    "coord_to_blender",
+    "look_at",
+    "homogeneous",
+    "gen_grid",
+    "get_image_to_tensor_balanced",
+    "get_mask_to_tensor",
+    "count_parameters",
+    "get_module",
+    "trans_t",
+    "rot_phi",
+    "rot_theta",
 ]
 
 
@@ -105,11 +132,15 @@ def _focal_c(width, height, focal, c):
     return fx, fy, cx, cy
 
 
-def gen_rays(poses, width, height, focal, z_near, z_far, c=None):
+def gen_rays(poses, width, height, focal, z_near, z_far, c=None, ndc=False):
     """Camera rays for every pixel of every pose: (NV, H, W, 8) (util.py:238-276).
 
     Poses on the HIP device run the ``pnr_gen_rays`` kernel (the rays are born in HBM);
-    host poses use the host restatement below, as the reference's host code does."""
+    host poses use the host restatement below, as the reference's host code does.
+    ``ndc=True`` is refused: the reference's NDC branch calls an ``ndc_rays`` its util module
+    does not define (util.py:254-262), so no caller can use it."""
+    if ndc:
+        raise NotImplementedError("gen_rays(ndc=True): the reference defines no ndc_rays (util.py:262)")
     if poses.is_cuda:
         from . import _lib
 
@@ -132,13 +163,13 @@ def gen_rays(poses, width, height, focal, z_near, z_far, c=None):
     return torch.cat((centers, dirs, nears, fars), dim=-1)
 
 
-def _trans_t(t):
+def trans_t(t):
     return torch.tensor(
         [[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, 1, t], [0, 0, 0, 1]], dtype=torch.float32
     )
 
 
-def _rot_phi(phi):
+def rot_phi(phi):
     return torch.tensor(
         [[1, 0, 0, 0],
          [0, np.cos(phi), -np.sin(phi), 0],
@@ -148,7 +179,7 @@ def _rot_phi(phi):
     )
 
 
-def _rot_theta(th):
+def rot_theta(th):
     return torch.tensor(
         [[np.cos(th), 0, -np.sin(th), 0],
          [0, 1, 0, 0],
@@ -160,9 +191,9 @@ def _rot_theta(th):
 
 def pose_spherical(theta, phi, radius):
     """Camera-to-world matrix on a sphere, NeRF convention (util.py:309-323)."""
-    c2w = _trans_t(radius)
-    c2w = _rot_phi(phi / 180.0 * np.pi) @ c2w
-    c2w = _rot_theta(theta / 180.0 * np.pi) @ c2w
+    c2w = trans_t(radius)
+    c2w = rot_phi(phi / 180.0 * np.pi) @ c2w
+    c2w = rot_theta(theta / 180.0 * np.pi) @ c2w
     flip = torch.tensor(
         [[-1, 0, 0, 0], [0, 0, 1, 0], [0, 1, 0, 0], [0, 0, 0, 1]], dtype=torch.float32
     )
@@ -173,3 +204,168 @@ def psnr(pred, target):
     """PSNR in dB of two tensors (util.py:474-481)."""
     mse = ((pred - target) ** 2).mean()
     return -10 * math.log10(float(mse))
+
+
+# ------------------------------------------------- the callers' other util.X helpers ----
+def batched_index_select_nd_last(t, inds):
+    """Gather along the last dim (util.py:45-55): t (..., n, m), inds (..., k) -> (..., n, k)."""
+    idx = inds.unsqueeze(-2).expand(*inds.shape[:-1], t.size(-2), inds.size(-1))
+    return t.gather(-1, idx)
+
+
+def masked_sample(masks, num_pix, prop_inside, thresh=0.5):
+    """(num_pix, 3) [view, row, col] picks, a share ``prop_inside`` from mask >= thresh
+    (util.py:205-217); draws inside picks, then outside picks, from torch's host generator."""
+    n_in = int(num_pix * prop_inside + 0.5)
+    inside = (masks >= thresh).nonzero(as_tuple=False)
+    outside = (masks < thresh).nonzero(as_tuple=False)
+    pick_in = inside[torch.randint(0, inside.shape[0], (n_in,))]
+    pick_out = outside[torch.randint(0, outside.shape[0], (num_pix - n_in,))]
+    return torch.cat((pick_in, pick_out))
+
+
+def get_cuda(gpu_id):
+    """``cuda:<gpu_id>`` when a HIP device is present, else the CPU device (util.py:193-202).
+    The ray march itself has no CPU path: a CPU net fails loudly at its first render."""
+    return torch.device("cuda:%d" % gpu_id) if torch.cuda.is_available() else torch.device("cpu")
+
+
+def image_float_to_uint8(img):
+    """Min-max stretch of a float image to uint8 (util.py:13-23; truncating cast)."""
+    lo, hi = np.min(img), np.max(img)
+    if hi - lo < 1e-10:
+        hi += 1e-10
+    out = (img - lo) / (hi - lo)
+    out *= 255.0
+    return out.astype(np.uint8)
+
+
+def _hot_lut():
+    """OpenCV's COLORMAP_HOT as a (256, 3) BGR uint8 table: the colormap is defined by 64 samples
+    of r = 5x/2, g = 5x/2 - 1, b = 5x - 4 (each clipped to [0, 1]; x = i/63), linearly interpolated
+    to 256 entries and scaled by 255 with rounding.  cv2 is absent offline, so the table is a
+    restatement of that definition, not pinned to cv2's own output (parity unpinned)."""
+    x = np.arange(64, dtype=np.float64) / 63.0
+    r = np.clip(2.5 * x, 0.0, 1.0)
+    g = np.clip(2.5 * x - 1.0, 0.0, 1.0)
+    b = np.clip(5.0 * x - 4.0, 0.0, 1.0)
+    xi = np.linspace(0.0, 1.0, 256)
+    rgb = np.stack([np.interp(xi, x, ch) for ch in (b, g, r)], -1)
+    return np.clip(np.rint(rgb * 255.0), 0, 255).astype(np.uint8)
+
+
+_HOT = None
+
+
+def cmap(img, color_map=None):
+    """HOT colouring of a float image (util.py:26-30: cv2.applyColorMap(image_float_to_uint8(img),
+    COLORMAP_HOT)): (H, W) or (H, W, 1) float -> (H, W, 3) uint8 in cv2's BGR channel order.
+    Only the HOT map is provided (the one the callers use, train.py:363-384)."""
+    global _HOT
+    if color_map not in (None, 11):   # cv2.COLORMAP_HOT == 11
+        raise NotImplementedError("util.cmap implements COLORMAP_HOT only")
+    if _HOT is None:
+        _HOT = _hot_lut()
+    u8 = image_float_to_uint8(np.asarray(img))
+    if u8.ndim == 3 and u8.shape[-1] == 1:
+        u8 = u8[..., 0]
+    return _HOT[u8]
+
+
+def quat_to_rot(q):
+    """(B, 4) quaternions [w, x, y, z] -> (B, 3, 3) rotations, normalising first (util.py:484-504)."""
+    q = torch.nn.functional.normalize(q, dim=1)
+    w, x, y, z = q.unbind(1)
+    rows = [1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y),
+            2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x),
+            2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]
+    return torch.stack(rows, 1).reshape(-1, 3, 3)
+
+
+def rot_to_quat(R):
+    """(B, 3, 3) rotations -> (B, 4) [w, x, y, z], the trace branch only (util.py:507-528)."""
+    w = torch.sqrt(1.0 + R[:, 0, 0] + R[:, 1, 1] + R[:, 2, 2]) / 2
+    return torch.stack((w, (R[:, 2, 1] - R[:, 1, 2]) / (4 * w), (R[:, 0, 2] - R[:, 2, 0]) / (4 * w),
+                        (R[:, 1, 0] - R[:, 0, 1]) / (4 * w)), 1)
+
+
+def coord_from_blender(dtype=torch.float32, device="cpu"):
+    """Blender axes (x right, y in, z up) -> x right, y up, z out (util.py:146-157)."""
+    return torch.tensor([[1, 0, 0, 0], [0, 0, 1, 0], [0, -1, 0, 0], [0, 0, 0, 1]], dtype=dtype, device=device)
+
+
+def coord_to_blender(dtype=torch.float32, device="cpu"):
+    """The inverse of coord_from_blender (util.py:160-171)."""
+    return torch.tensor([[1, 0, 0, 0], [0, 0, -1, 0], [0, 1, 0, 0], [0, 0, 0, 1]], dtype=dtype, device=device)
+
+
+def look_at(origin, target, world_up=np.array([0, 1, 0], dtype=np.float32)):
+    """4 x 4 camera-to-world matrix of a camera at ``origin`` looking at ``target`` (util.py:174-190)."""
+    back = origin - target
+    back = back / np.linalg.norm(back)
+    right = np.cross(world_up, back)
+    right = right / np.linalg.norm(right)
+    up = np.cross(back, right)
+    m = np.zeros((4, 4), dtype=np.float32)
+    m[:3, 0], m[:3, 1], m[:3, 2], m[:3, 3] = right, up, back, origin
+    m[3, 3] = 1.0
+    return m
+
+
+def homogeneous(points):
+    """Append a 1 to every point: (..., 3) -> (..., 4) (util.py:84-90)."""
+    return torch.nn.functional.pad(points, (0, 1), "constant", 1.0)
+
+
+def gen_grid(*args, ij_indexing=False):
+    """Points of a grid with one (lo, hi, n) per dimension, (prod n, len(args)) (util.py:93-110)."""
+    axes = [np.linspace(lo, hi, n, dtype=np.float32) for lo, hi, n in args]
+    mesh = np.meshgrid(*axes, indexing="ij" if ij_indexing else "xy")
+    return torch.from_numpy(np.vstack(mesh).reshape(len(args), -1).T)
+
+
+class _ToTensorNormalize:
+    """torchvision ToTensor() + Normalize(mean, std) (+ an optional Resize of the shorter edge)
+    for (H, W, C) uint8 arrays or PIL images -> (C, H, W) float32 (torchvision is absent)."""
+
+    def __init__(self, mean, std, image_size=0):
+        self.mean, self.std, self.size = float(mean), float(std), image_size
+
+    def __call__(self, img):
+        if self.size and self.size > 0:
+            from PIL import Image
+
+            im = img if isinstance(img, Image.Image) else Image.fromarray(np.asarray(img))
+            w, h = im.size
+            if w <= h:
+                nw, nh = self.size, int(self.size * h / w)
+            else:
+                nw, nh = int(self.size * w / h), self.size
+            img = im.resize((nw, nh), Image.BILINEAR)
+        a = np.asarray(img)
+        if a.ndim == 2:
+            a = a[..., None]
+        t = torch.from_numpy(np.ascontiguousarray(a)).permute(2, 0, 1).float()
+        if a.dtype == np.uint8:
+            t = t.div(255.0)
+        return (t - self.mean) / self.std
+
+
+def get_image_to_tensor_balanced(image_size=0):
+    """ToTensor + Normalize(0.5, 0.5): uint8 image -> [-1, 1] (util.py:68-75)."""
+    return _ToTensorNormalize(0.5, 0.5, image_size)
+
+
+def get_mask_to_tensor():
+    """ToTensor + Normalize(0, 1): uint8 mask -> [0, 1] (util.py:78-81)."""
+    return _ToTensorNormalize(0.0, 1.0)
+
+
+def count_parameters(model):
+    """Trainable parameter count (util.py:326-327)."""
+    return sum(p.numel() for p in model.parameters() if p.requires_grad)
+
+
+def get_module(net):
+    """``net.module`` of a DataParallel wrapper, else ``net`` (util.py:531-538)."""
+    return net.module if isinstance(net, torch.nn.DataParallel) else net

@@ -476,3 +476,46 @@ def test_weight_grad_arith_selects_kernel():
     arr = (ctypes.c_void_p * 1)(d.data_ptr())
     rc = lib.pnr_weight_grad_arith(arr, arr, arr, 1, P, 7, None, 0, None)
     assert rc == -1 and b"arithmetic" in lib.pnr_last_error()
+
+
+@pytest.mark.parametrize("coarse", [True, False])
+@pytest.mark.parametrize("precision", ["fp32", "f16x3"])
+def test_grad_point_query_matches_oracle_autograd(precision, coarse):
+    """The reference's callers query the net WITHOUT torch.no_grad() (eval/eval.py:100, the density
+    grid; train/train.py:422): the output carries the autograd graph.  Here that query runs the
+    training forward (PixelNeRFNet._forward_points_grad -> train.RenderPoints at z = 0); its values
+    and its gradients (MLP parameters and latent, SB = 2 objects) against the oracle's autograd, at
+    the training tests' tolerance."""
+    cs = case(sb=2, rays_per_obj=8, seed=7)
+    xyz = torch.from_numpy(synth.hash_sym(81, (2, 300, 3), 0.5))
+    vd = torch.nn.functional.normalize(torch.from_numpy(synth.hash_sym(82, (2, 300, 3), 1.0)), dim=-1)
+    wt = torch.from_numpy(synth.hash_sym(83, (2, 300, 4), 1.0))
+    sd = dict(cs["sd"])
+    params = {k: v.clone().requires_grad_(True) for k, v in sd.items() if k.startswith("mlp_")}
+    sd.update(params)
+    latent = cs["latent"].clone().requires_grad_(True)
+    scene = ref_cpu.Scene(latent, cs["poses"][:, None], cs["focal"], cs["width"], cs["height"], cs["c"])
+    ref = ref_cpu.pixelnerf_forward(sd, scene, xyz, coarse, vd)
+    (ref * wt).sum().backward()
+    net = PixelNeRFNet(conf())
+    net.load_state_dict(cs["sd"], strict=False)
+    net = net.to(DEV)
+    net.mlp_precision = precision
+    lat_d = cs["latent"].to(DEV).requires_grad_(True)
+    net.encode_latent(lat_d, cs["poses"].to(DEV), cs["focal"].to(DEV), (cs["width"], cs["height"]),
+                      c=cs["c"].to(DEV), num_objs=2)
+    out = net(xyz.to(DEV), coarse=coarse, viewdirs=vd.to(DEV))
+    assert out.requires_grad and out.grad_fn is not None
+    d = (out.detach().cpu() - ref.detach()).abs()
+    assert bool((d <= 5e-5 + 1e-5 * ref.detach().abs()).all()), float(d.max())
+    (out * wt.to(DEV)).sum().backward()
+    tol = 1e-4 if precision == "fp32" else 2e-4
+    used = "mlp_coarse." if (coarse or net.mlp_fine is None) else "mlp_fine."
+    got = {k: p.grad.detach().cpu() for k, p in net.named_parameters() if k.startswith(used)}
+    exp = {k: p.grad for k, p in params.items() if k.startswith(used)}
+    got["latent"], exp["latent"] = lat_d.grad.detach().cpu(), latent.grad
+    assert set(got) == set(exp), set(got) ^ set(exp)
+    for k in sorted(exp):
+        a, b = got[k].reshape(-1).double(), exp[k].reshape(-1).double()
+        scale = float(b.abs().max())
+        assert float((a - b).abs().max()) <= tol * scale + 1e-9, k

@@ -96,10 +96,14 @@ def test_encode_builds_camera_records():
         net(torch.zeros(2, 4, 3), coarse=True, viewdirs=torch.zeros(2, 4, 3))
 
 
-def test_forward_only_guard():
+def test_grad_point_query_routes_to_training_forward_and_refuses_cpu():
+    """eval/eval.py:100 and train/train.py:422 query the net with grad enabled: the query builds
+    its autograd graph through train.RenderPoints (tests/test_gpu_parity.py checks its values and
+    gradients on the device); CPU tensors are refused loudly, as on every HIP path."""
     net = make_model(_conf_dict())
     net.encode_latent(torch.zeros(1, 512, 4, 4), synth.srn_poses([0.0]), torch.tensor(50.0), (32, 32))
-    with pytest.raises(NotImplementedError, match="forward-only"):
+    assert torch.is_grad_enabled() and net.needs_grad()
+    with pytest.raises(ValueError, match="HIP device"):
         net(torch.zeros(1, 2, 3), coarse=True, viewdirs=torch.zeros(1, 2, 3))
 
 
