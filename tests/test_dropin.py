@@ -168,6 +168,9 @@ def ref_tree(tmp_path_factory):
     for i, stage in enumerate(("train", "val", "test")):
         srn_synth.write_srn_dir(str(root / "data"), srn_synth.make_inputs(n_obj=2, n_views=3, size=32, seed=i),
                                 stage=stage)
+    import dvr_synth
+
+    dvr_synth.write_dvr_dir(str(root / "nmr"), dvr_synth.make_dvr_inputs("shapenet", size=32), stage="test")
     return root
 
 
@@ -195,6 +198,16 @@ DATA = ["-F", "srn", "-D", "data/cars"]
 def test_gen_video_runs_unchanged_up_to_the_render(ref_tree):
     r = _run(ref_tree, "eval/gen_video.py", "-n", "srn_car", *DATA, "--split", "test", "-S", "0", "-P", "0",
              "--num_views", "2")
+    assert "Encoding source view(s)" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    _stops_at_render(r, "eval/gen_video.py", "render_par(rays[None])")
+
+
+@needs_ref
+def test_gen_video_on_nmr_layout_runs_unchanged_up_to_the_render(ref_tree):
+    """The headline workload's caller (BASELINE cfg3): gen_video.py with the sn64 conf on
+    DVR-layout ShapeNet-NMR data (-F dvr, the reference's default format)."""
+    r = _run(ref_tree, "eval/gen_video.py", "-n", "sn64", "-F", "dvr", "-D", "nmr/dvr", "--split", "test", "-S", "1",
+             "-P", "0", "--num_views", "2")
     assert "Encoding source view(s)" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
     _stops_at_render(r, "eval/gen_video.py", "render_par(rays[None])")
 
