@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 5   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
-                               5: pnr_latent_channels_last_nhwc */
+#define PNR_ABI_VERSION 6   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
+                               5: pnr_latent_channels_last_nhwc;
+                               6: pnr_fold_batchnorm */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -318,6 +319,26 @@ int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *chann
                                   const int32_t *heights, const int32_t *widths, int32_t n_maps,
                                   int32_t n_images, float *latent_cl, int32_t out_h, int32_t out_w,
                                   pnr_stream_t stream);
+
+/* One (convolution, BatchNorm) pair of the eval-mode encoder trunk (encoder.py:135-149 with the
+ * BatchNorms on their running statistics).  conv_w / w_out: n_out blocks of per_out contiguous
+ * floats (OIHW or channels-last OHWI weights: the output channel is outermost in both); gamma /
+ * beta NULL for a BatchNorm without affine parameters. */
+typedef struct pnr_bn_fold {
+    const float *conv_w;
+    const float *gamma, *beta, *mean, *var;
+    float *w_out, *b_out;
+    int64_t n_out, per_out;
+    float eps;
+    int32_t pad_;
+} pnr_bn_fold;
+
+/* Fold every pair: w_out[o, :] = conv_w[o, :] s[o], b_out[o] = beta[o] - mean[o] s[o] with
+ * s = gamma[o] / sqrt(var[o] + eps) (correctly rounded sqrt and divide).  `folds` is a DEVICE
+ * array of n_folds records (the kernel reads it; a HIP graph that captured this call keeps
+ * reading the same array); max_elems = max n_out * per_out.  Replaces the per-encode BatchNorm
+ * arithmetic of SpatialEncoder.forward in eval mode (encoder.py:135-149); ABI 6. */
+int pnr_fold_batchnorm(const pnr_bn_fold *folds, int32_t n_folds, int64_t max_elems, pnr_stream_t stream);
 
 /* ---- training (autograd over the ray march) ------------ */
 /* Floats of the activation save of pnr_render_points for n_points rows; call it with

@@ -34,6 +34,7 @@ size_t mlp_bwd_workspace_bytes(const pnr_mlp_desc &, int64_t);
 size_t wgrad_workspace_bytes(int, int64_t);
 int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
                  hipStream_t, int arith);
+int launch_fold_bn(const pnr_bn_fold *, int, int64_t, hipStream_t);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
                      int, int, bool, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
@@ -599,6 +600,12 @@ int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *chann
         return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_nhwc: bad sizes");
     return launch_latent_cl(maps, channels, heights, widths, n_maps, n_images, latent_cl, out_h, out_w, true,
                             (hipStream_t)stream);
+}
+
+int pnr_fold_batchnorm(const pnr_bn_fold *folds, int32_t n_folds, int64_t max_elems, pnr_stream_t stream) {
+    if (n_folds < 0 || n_folds > 65535 || max_elems < 0) return fail(PNR_ERR_INVALID, "pnr_fold_batchnorm: bad sizes");
+    if (n_folds > 0 && !folds) return fail(PNR_ERR_INVALID, "pnr_fold_batchnorm: NULL");
+    return launch_fold_bn(folds, n_folds, max_elems, (hipStream_t)stream);
 }
 
 int pnr_gen_rays(const float *poses, int64_t n_images, int32_t pose_rows, int32_t width, int32_t height,

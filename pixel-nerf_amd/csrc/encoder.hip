@@ -87,4 +87,32 @@ int launch_latent_cl(const float *const *maps, const int32_t *channels, const in
     return launch_ok("latent_cl") ? PNR_OK : PNR_ERR_HIP;
 }
 
+// BatchNorm folded into the convolution before it, for the eval-mode trunk (pnr.encoder.InferenceTrunk):
+// W'[o, :] = W[o, :] s[o], b'[o] = beta[o] - mean[o] s[o], s = gamma / sqrt(var + eps) (gamma 1 and
+// beta 0 when the BatchNorm has no affine parameters).  One launch folds every (conv, bn) pair of
+// the trunk from their live storage (blockIdx.y = pair), so the HIP graph that replays the trunk
+// refolds on every replay and in-place edits of any weight or statistic are always seen.
+__global__ __launch_bounds__(256) void k_fold_bn(const pnr_bn_fold *__restrict__ folds) {
+    const pnr_bn_fold f = folds[blockIdx.y];
+    const int64_t n = f.n_out * f.per_out;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = e / f.per_out;
+        const float inv = __fdiv_rn(1.f, __fsqrt_rn(add_rn(f.var[o], f.eps)));
+        const float s = f.gamma ? mul_rn(f.gamma[o], inv) : inv;
+        f.w_out[e] = mul_rn(f.conv_w[e], s);
+        if (e - o * f.per_out == 0) {
+            const float beta = f.beta ? f.beta[o] : 0.f;
+            f.b_out[o] = sub_rn(beta, mul_rn(f.mean[o], s));
+        }
+    }
+}
+
+int launch_fold_bn(const pnr_bn_fold *folds, int n_folds, int64_t max_elems, hipStream_t st) {
+    if (n_folds == 0 || max_elems == 0) return PNR_OK;
+    const int64_t blocks = (max_elems + 255) / 256;
+    const dim3 grid((unsigned)(blocks < 256 ? blocks : 256), (unsigned)n_folds);
+    hipLaunchKernelGGL(k_fold_bn, grid, dim3(256), 0, st, folds);
+    return launch_ok("fold_bn") ? PNR_OK : PNR_ERR_HIP;
+}
+
 }  // namespace pnr

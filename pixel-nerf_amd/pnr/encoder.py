@@ -79,63 +79,102 @@ class LatentChannelsLast(torch.autograd.Function):
         return tuple(grads)
 
 
+class _BnFold(ctypes.Structure):
+    """include/pnr_abi.h pnr_bn_fold."""
+    _fields_ = [("conv_w", ctypes.c_void_p), ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p),
+                ("mean", ctypes.c_void_p), ("var", ctypes.c_void_p), ("w_out", ctypes.c_void_p),
+                ("b_out", ctypes.c_void_p), ("n_out", ctypes.c_int64), ("per_out", ctypes.c_int64),
+                ("eps", ctypes.c_float), ("pad_", ctypes.c_int32)]
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
 class InferenceTrunk:
     """The encoder trunk for rendering (eval mode, no autograd; encoder.py:135-164's forward with
     the BatchNorms on their running statistics, what gen_video.py / eval.py run after .eval()):
 
     * every BatchNorm is folded into the convolution before it, W' = W s and b' = beta - mu s with
-      s = gamma / sqrt(var + eps) per output channel (the same affine map, one rounding apart);
+      s = gamma / sqrt(var + eps) per output channel (the same affine map, one rounding apart), by
+      ONE ``pnr_fold_batchnorm`` launch over all pairs at the head of every encode;
     * ReLUs and residual adds run in place;
-    * the trunk and the channels-last latent kernel (``pnr_latent_channels_last``) are captured
-      once per input shape as one HIP graph and replayed: the eval encode is ~140 small launches
-      whose host-side issue, not their GPU time, sets its duration (the fixed per-rank cost at
-      N = 8).
+    * the fold, the trunk and the channels-last latent kernel (``pnr_latent_channels_last``) are
+      captured once per input shape as one HIP graph and replayed: the eval encode is ~140 small
+      launches whose host-side issue, not their GPU time, sets its duration (the fixed per-rank
+      cost at N = 8).
 
-    The folded weights are recomputed in place (the graph reads the same buffers) whenever a
-    convolution weight, BatchNorm parameter or running statistic changed (tensor versions and
-    storage), so optimizer steps and load_state_dict are seen."""
+    Because the fold runs inside every replay from the live storage of the convolution weights and
+    BatchNorm tensors, every in-place change is seen -- optimizer steps, ``load_state_dict``,
+    ``p.data.copy_`` (which a tensor version counter does not record).  The (conv, bn) pairs and
+    their storage pointers are re-read from the module on every encode: a replaced tensor
+    (``load_state_dict(assign=True)``) or a swapped module rebuilds the fold table, and a changed
+    shape drops the captured graphs.  ``SpatialEncoder.invalidate_inference_cache()`` drops
+    everything explicitly."""
 
     def __init__(self, enc, device):
         self.owner = weakref.ref(enc)
         self.device = device
-        m = enc.model
-        self.layers = [m.layer1, m.layer2, m.layer3, m.layer4][:max(enc.num_layers - 1, 0)]
+        self.key = None
+        self.folded = []          # per pair position: (w', b')
+        self.table = None         # device copy of the pnr_bn_fold records
+        self.n_folds, self.max_elems = 0, 0
+        self.graphs = {}          # (shape, dtype, strides) -> (graph, static input, static latent)
+        self.use_graph = True
+
+    def _pairs(self):
+        m = self.owner().model
+        self.layers = [m.layer1, m.layer2, m.layer3, m.layer4][:max(self.owner().num_layers - 1, 0)]
         pairs = [(m.conv1, m.bn1)]
         for layer in self.layers:
             for blk in layer:
                 pairs += [(blk.conv1, blk.bn1), (blk.conv2, blk.bn2)]
                 if blk.downsample is not None:
                     pairs.append((blk.downsample[0], blk.downsample[1]))
-        self.pairs = pairs
-        self.folded = {id(c): (torch.empty_like(c.weight), torch.empty(c.out_channels, device=device))
-                       for c, _ in pairs}
-        self.tensors = list(self._tensors())
-        self.key = None
-        self.graphs = {}          # (shape, dtype, strides) -> (graph, static input, static latent)
-        self.use_graph = True
-
-    def _tensors(self):
-        for c, b in self.pairs:
-            yield c.weight
-            for t in (b.weight, b.bias, b.running_mean, b.running_var):
-                if t is not None:
-                    yield t
+        return pairs
 
     def refresh(self):
-        # versions of every folded-in tensor (in-place updates) and the conv weights' storage
-        # (replaced data); ~30 us per encode
-        key = (tuple(t._version for t in self.tensors), tuple(c.weight.data_ptr() for c, _ in self.pairs))
+        """Re-read the (conv, bn) pairs from the module; rebuild the fold table when any tensor
+        object, storage or eps changed (~40 us of host work per encode)."""
+        pairs = self._pairs()
+        self.pairs = pairs
+        key = tuple((id(c), _ptr(c.weight), _ptr(b.weight), _ptr(b.bias), _ptr(b.running_mean),
+                     _ptr(b.running_var), float(b.eps)) for c, b in pairs)
         if key == self.key:
             return
-        with torch.no_grad():
-            for c, b in self.pairs:
-                w, bias = self.folded[id(c)]
-                s = torch.rsqrt(b.running_var + b.eps)
-                if b.weight is not None:
-                    s = s * b.weight
-                w.copy_(c.weight * s.view(-1, 1, 1, 1))
-                bias.copy_(-b.running_mean * s if b.bias is None else b.bias - b.running_mean * s)
+        for i, (c, b) in enumerate(pairs):
+            w = c.weight
+            if w.dtype != torch.float32 or w.device != self.device or not (
+                    w.is_contiguous() or w.is_contiguous(memory_format=torch.channels_last)):
+                raise ValueError("pnr: encoder conv weights must be dense fp32 on %s" % self.device)
+            if i >= len(self.folded) or self.folded[i][0].shape != w.shape or self.folded[i][0].stride() != w.stride():
+                if i < len(self.folded):
+                    self.folded[i] = None
+                else:
+                    self.folded.append(None)
+                self.graphs.clear()   # the captured convolutions read the old buffers
+            if self.folded[i] is None:
+                self.folded[i] = (torch.empty_like(w), torch.empty(c.out_channels, device=self.device))
+        del self.folded[len(pairs):]
+        recs = (_BnFold * len(pairs))()
+        for i, (c, b) in enumerate(pairs):
+            w_out, b_out = self.folded[i]
+            recs[i] = _BnFold(_ptr(c.weight), _ptr(b.weight), _ptr(b.bias), _ptr(b.running_mean), _ptr(b.running_var),
+                              _ptr(w_out), _ptr(b_out), c.out_channels, c.weight[0].numel(), float(b.eps), 0)
+        host = torch.frombuffer(bytearray(bytes(recs)), dtype=torch.uint8)
+        if self.table is None or self.table.numel() != host.numel():
+            self.table = torch.empty(host.numel(), dtype=torch.uint8, device=self.device)
+            self.graphs.clear()   # the captured fold reads the old table
+        self.table.copy_(host)    # stream-ordered before the next fold (a replay reads it in place)
+        self.n_folds = len(pairs)
+        self.max_elems = max(c.weight.numel() for c, _ in pairs)
         self.key = key
+
+    def fold(self):
+        from . import _lib
+
+        _lib.check(_lib.load().pnr_fold_batchnorm(self.table.data_ptr(), self.n_folds, self.max_elems,
+                                                  _lib.stream_of(self.device)), "pnr_fold_batchnorm")
 
     # conv + bias + relu and conv + bias + residual + relu as MIOpen's fused forward ops
     # (torch.miopen_convolution_relu / _add_relu); False: F.conv2d + in-place relu / add.
@@ -147,8 +186,9 @@ class InferenceTrunk:
     def trunk(self, x):
         enc = self.owner()
         m = enc.model
-        f = self.folded
+        f = {id(c): wb for (c, _), wb in zip(self.pairs, self.folded)}
         fused = self.fused
+        self.fold()
 
         def conv(c, x, relu=True, add=None):
             w, b = f[id(c)]
@@ -315,6 +355,18 @@ class SpatialEncoder(nn.Module):
         # eval-mode encodes on the device run the folded, graph-replayed trunk (InferenceTrunk)
         self.infer_fast = True
         self._infer = None
+
+    def invalidate_inference_cache(self):
+        """Drop the eval-mode inference trunk (its fold table and captured HIP graphs); the next
+        eval-mode encode rebuilds it from the module as it is then."""
+        self._infer = None
+
+    def __getstate__(self):
+        # the inference trunk holds HIP graphs and a weak reference: never copied or pickled
+        # (copy.deepcopy / pickle of an encoded model); a copy rebuilds its own on first use
+        state = super().__getstate__().copy()
+        state["_infer"] = None
+        return state
 
     def set_latent(self, latent):
         """Install a feature map (NS, C, H_l, W_l) as forward() would (encoder.py:160-163)."""

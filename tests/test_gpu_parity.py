@@ -862,6 +862,44 @@ def test_eval_encode_inference_trunk_matches_module_path():
     got3, _ = encode(imgs[0], True)
     assert not torch.equal(got3, first)
     check(got3, ref3)
+    # updates a version-counter key cannot see: through .data, a replaced tensor
+    # (load_state_dict(assign=True)), a swapped module; each against the module path
+    prev = got3
+
+    def changed():
+        nonlocal prev
+        ref = encode(imgs[0], False)[0]
+        got, _ = encode(imgs[0], True)
+        assert not torch.equal(got, prev)
+        check(got, ref)
+        prev = got
+
+    with torch.no_grad():
+        w = enc.model.layer1[1].conv2.weight
+        w.data.copy_(w * 1.5)
+    changed()
+    with torch.no_grad():
+        enc.model.layer3[2].bn1.running_var.data.mul_(3.0)
+    changed()
+    n_graphs = len(enc._infer.graphs)
+    sd = {k: (v * 1.1 if k.endswith("bn1.weight") else v).clone() for k, v in enc.state_dict().items()}
+    enc.load_state_dict(sd, assign=True)
+    changed()
+    assert len(enc._infer.graphs) == n_graphs    # same shapes: the graph is kept, the table rewritten
+    bn = torch.nn.BatchNorm2d(128, eps=1e-3).to(DEV).eval()
+    with torch.no_grad():
+        bn.running_mean.copy_(torch.randn(128, generator=g).to(DEV) * 0.1)
+        bn.running_var.copy_((torch.rand(128, generator=g) + 0.5).to(DEV))
+    enc.model.layer2[0].bn2 = bn
+    changed()
+    import copy
+
+    twin = copy.deepcopy(enc)                    # an encoded model copies without its graphs
+    assert twin._infer is None
+    twin.infer_fast = True
+    with torch.no_grad():
+        twin(imgs[1])
+    check(twin.latent_cl, encode(imgs[1], False)[0])
 
 
 # ----------------------------------------------------- coarse-output reuse --

@@ -290,40 +290,47 @@ def test_callback_confs_and_state_dict_layout():
     assert PixelNeRFNet(cases["viewdirs"]).d_in == 78
 
 
-def test_inference_trunk_folds_batchnorm():
-    """pnr.encoder.InferenceTrunk (the eval-mode encode): every folded convolution equals the
-    module's conv + BatchNorm on its running statistics (CPU tensors; the graph replay and the
-    latent kernel are covered by test_gpu_parity), the fold follows in-place parameter updates,
-    and CPU tensors or train mode keep the module path."""
-    import torch.nn.functional as F
-    from pnr.encoder import InferenceTrunk, SpatialEncoder
+def test_inference_trunk_fold_table_follows_the_module():
+    """pnr.encoder.InferenceTrunk (the eval-mode encode) builds its pnr_fold_batchnorm records from
+    the LIVE module on every encode: one record per (conv, bn) pair with the tensors' current
+    storage, and a new table when a tensor is replaced (load_state_dict(assign=True)) or a module
+    swapped -- the cases a version-counter key misses.  The fold arithmetic itself and
+    the graph replay run on the device (tests/test_gpu_parity.py::test_eval_encode_*); a deepcopy /
+    pickle of an encoder never carries the trunk's graphs."""
+    import copy
+    import pickle
 
-    g = torch.Generator().manual_seed(0)
-    enc = SpatialEncoder(pretrained=False)
-    for mod in enc.modules():
-        if isinstance(mod, torch.nn.BatchNorm2d):
-            c = mod.num_features
-            mod.running_mean.copy_(torch.randn(c, generator=g))
-            mod.running_var.copy_(torch.rand(c, generator=g) + 0.1)
-            mod.weight.data.copy_(torch.randn(c, generator=g))
-            mod.bias.data.copy_(torch.randn(c, generator=g))
-    enc.eval()
+    from pnr.encoder import InferenceTrunk, SpatialEncoder, _BnFold
+
+    enc = SpatialEncoder(pretrained=False).eval()
     t = InferenceTrunk(enc, torch.device("cpu"))
     t.refresh()
     assert len(t.pairs) == 1 + 2 * (3 + 4 + 6) + 2   # conv1, layer1-3 blocks, 2 downsamples
+
+    def records():
+        return (_BnFold * len(t.pairs)).from_buffer_copy(t.table.numpy().tobytes())
+
+    for r, (conv, bn), (w_out, b_out) in zip(records(), t.pairs, t.folded):
+        assert r.conv_w == conv.weight.data_ptr() and r.var == bn.running_var.data_ptr()
+        assert r.gamma == bn.weight.data_ptr() and r.w_out == w_out.data_ptr() and r.b_out == b_out.data_ptr()
+        assert (r.n_out, r.per_out) == (conv.out_channels, conv.weight[0].numel()) and abs(r.eps - bn.eps) < 1e-12
+        assert w_out.shape == conv.weight.shape and w_out.stride() == conv.weight.stride()
+    assert t.max_elems == max(c.weight.numel() for c, _ in t.pairs)
+    key = t.key
     with torch.no_grad():
-        for conv, bn in t.pairs:
-            x = torch.randn(1, conv.in_channels, 12, 12, generator=g)
-            w, b = t.folded[id(conv)]
-            got = F.conv2d(x, w, b, conv.stride, conv.padding)
-            want = bn(conv(x))
-            assert (got - want).abs().max() <= 1e-4 * want.abs().max(), conv
-        enc.model.layer3[0].bn1.bias.add_(1.0)
+        enc.model.layer1[0].conv1.weight.data.copy_(torch.randn_like(enc.model.layer1[0].conv1.weight))
     t.refresh()
-    conv, bn = next(p for p in t.pairs if p[1] is enc.model.layer3[0].bn1)
-    x = torch.randn(1, conv.in_channels, 8, 8, generator=g)
-    with torch.no_grad():
-        got = F.conv2d(x, *t.folded[id(conv)], conv.stride, conv.padding)
-        assert (got - bn(conv(x))).abs().max() <= 1e-4 * got.abs().max()
-    with torch.no_grad():
-        assert not enc._use_infer(torch.zeros(1, 3, 8, 8))      # CPU input: module path
+    assert t.key == key   # same storage: the in-kernel fold reads the new values on the next replay
+    sd = {k: v.clone() for k, v in enc.state_dict().items()}
+    enc.load_state_dict(sd, assign=True)
+    t.refresh()
+    assert t.key != key and records()[0].conv_w == enc.model.conv1.weight.data_ptr()
+    enc.model.layer3[0].bn1 = torch.nn.BatchNorm2d(256, eps=1e-3)   # a swapped module
+    t.refresh()
+    i = next(k for k, (_, b) in enumerate(t.pairs) if b is enc.model.layer3[0].bn1)
+    assert abs(records()[i].eps - 1e-3) < 1e-9 and records()[i].var == enc.model.layer3[0].bn1.running_var.data_ptr()
+    enc._infer = t
+    assert copy.deepcopy(enc)._infer is None and enc._infer is t
+    assert pickle.loads(pickle.dumps(enc))._infer is None
+    enc.invalidate_inference_cache()
+    assert enc._infer is None
