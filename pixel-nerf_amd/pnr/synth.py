@@ -113,6 +113,26 @@ def pixelnerf_state(seed, d_in=42, d_latent=512, d_hidden=512, n_blocks=5,
     return sd
 
 
+def encoder_state(seed, template):
+    """Hash-initialised values for an encoder trunk state dict ``template`` (name -> tensor), in the
+    template's order: convolutions U(-1, 1) sqrt(3 / fan_in) (unit-variance activations), BatchNorm
+    gamma U(0.5, 1.5), beta U(-0.1, 0.1), running_mean U(-0.2, 0.2), running_var U(0.5, 2.0)
+    (non-trivial statistics, so the BatchNorm arithmetic is exercised), num_batches_tracked 0."""
+    out = {}
+    for i, (k, v) in enumerate(template.items()):
+        s = seed * 1000 + i
+        if k.endswith("num_batches_tracked"):
+            out[k] = torch.zeros_like(v)
+        elif v.dim() == 4:
+            out[k] = torch.from_numpy(hash_sym(s, tuple(v.shape), float(np.sqrt(3.0 / v[0].numel()))))
+        else:
+            lo, hi = {"weight": (0.5, 1.5), "bias": (-0.1, 0.1), "running_mean": (-0.2, 0.2),
+                      "running_var": (0.5, 2.0)}[k.rsplit(".", 1)[1]]
+            u = hash_uniform(s, v.numel()).astype(np.float32).reshape(tuple(v.shape))
+            out[k] = torch.from_numpy(lo + (hi - lo) * u)
+    return out
+
+
 def latent(seed, n_views, channels, h_l, w_l):
     """(NS, C, H_l, W_l) float32 latent, channels-first as the encoder emits it."""
     return torch.from_numpy(hash_normal(seed, (n_views, channels, h_l, w_l)))

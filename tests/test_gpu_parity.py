@@ -9,6 +9,7 @@ coarse weights (oracle/parity.py: the bins recomputed from the HIP and the
 reference coarse weights with the same u differ); every differing fine sample set
 must be such a ray, and at most MAX_FLIPS rays per fixture may flip.
 """
+import numpy as np
 import pytest
 import torch
 
@@ -1244,3 +1245,48 @@ def test_single_launch_uses_each_pack_pe_table():
                                  zf, rays, B, 64, 64, 0, 0.01, True, False, None, None, None, None, 1234, 0, True,
                                  True, [], 0)
     assert not torch.equal(other[3], outs[0][3])
+
+
+# ----------------------------------------------------- encoder vs the reference --
+@pytest.mark.parametrize("layout", ["nhwc", "nchw"])
+@pytest.mark.parametrize("fast", [False, True])
+def test_encode_matches_reference_encoder_fixture(fast, layout):
+    """PixelNeRFNet.encode's latent against the REFERENCE's SpatialEncoder.forward (encoder.py:111-164,
+    tests/golden/encoder_fw.npz made by tests/golden/make_encoder_golden.py on the same hashed
+    weights): every eval case (use_first_pool, num_layers 3 / 4, feature_scale 1 / 0.5) through the
+    module path (fast False) and the BN-folded graph-replayed trunk (fast True), with the trunk in
+    channels-last (the default) and NCHW memory format; the train-mode case (batch statistics) on
+    the module path.  Tolerance 2e-5 of the latent's range (MIOpen vs CPU convolution order) and
+    latent_scaling exact."""
+    import json
+    import os
+
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "encoder_fw.npz")))
+    cases = json.loads(bytes(g["cases"]).decode())
+    imgs = torch.from_numpy(g["images"]).to(DEV)
+    for i, c in enumerate(cases):
+        if c["train"] and fast:
+            continue   # the folded trunk is eval-only
+        conf = model_conf()
+        conf["encoder"] = dict(backbone="resnet34", pretrained=False, num_layers=c["num_layers"],
+                               feature_scale=c["feature_scale"], use_first_pool=c["use_first_pool"])
+        net = PixelNeRFNet(conf)
+        net.encoder.model.load_state_dict(synth.encoder_state(int(g["weight_seed"]), net.encoder.model.state_dict()))
+        if layout == "nchw":
+            net.encoder.model.to(memory_format=torch.contiguous_format)
+        net = net.to(DEV)
+        net.train(c["train"])
+        net.encoder.infer_fast = fast
+        x = imgs if c["train"] else imgs[:1]
+        poses = synth.srn_poses([0.0] * x.shape[0]).to(DEV)
+        with torch.no_grad():
+            net.encode(x, poses, torch.tensor(30.0, device=DEV))
+        lat = net.encoder.latent.detach().cpu()
+        ref = torch.from_numpy(g["latent_%d" % i])
+        assert lat.shape == ref.shape, (c, lat.shape)
+        scale = float(ref.abs().max())
+        d = float((lat - ref).abs().max())
+        assert d <= (5e-5 if c["train"] else 2e-5) * scale, (c, fast, layout, d, scale)
+        assert torch.equal(net.encoder.latent_scaling.cpu(), torch.from_numpy(g["latent_scaling_%d" % i])), c
+        # the channels-last copy the ray march gathers from is the same latent
+        assert torch.equal(net.encoder.latent_cl.cpu(), lat.permute(0, 2, 3, 1)), c

@@ -485,8 +485,11 @@ def test_grad_point_query_matches_oracle_autograd(precision, coarse):
     grid; train/train.py:422): the output carries the autograd graph.  Here that query runs the
     training forward (PixelNeRFNet._forward_points_grad -> train.RenderPoints at z = 0); its values
     and its gradients (MLP parameters and latent, SB = 2 objects) against the oracle's autograd, at
-    the training tests' tolerance."""
+    the training tests' tolerance, on `conditioned` weights (no ReLU within rounding of its kink:
+    on the raw hash weights the f16x3 forward flips a few units the fp32 oracle does not, and each
+    flip moves the latent gradient below it by ~1e-3 of its range, as the training tests found)."""
     cs = case(sb=2, rays_per_obj=8, seed=7)
+    cs["sd"] = conditioned(cs["sd"])
     xyz = torch.from_numpy(synth.hash_sym(81, (2, 300, 3), 0.5))
     vd = torch.nn.functional.normalize(torch.from_numpy(synth.hash_sym(82, (2, 300, 3), 1.0)), dim=-1)
     wt = torch.from_numpy(synth.hash_sym(83, (2, 300, 4), 1.0))

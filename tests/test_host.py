@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 import torch
 
@@ -34,7 +35,8 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.pnr_abi_version() == 5
+    assert lib.pnr_abi_version() == 6
+    assert lib.pnr_fold_batchnorm(None, 3, 10, None) == -1 and b"NULL" in lib.pnr_last_error()
     # an invalid call fails with a message, without touching the GPU
     rc = lib.pnr_composite(None, None, None, 4, 0, 0, None, None, None, None)
     assert rc == -1
@@ -334,3 +336,80 @@ def test_inference_trunk_fold_table_follows_the_module():
     assert pickle.loads(pickle.dumps(enc))._infer is None
     enc.invalidate_inference_cache()
     assert enc._infer is None
+
+
+def _torchvision_resnet34_keys():
+    """torchvision.models.resnet34's state-dict names and shapes (BasicBlock x [3, 4, 6, 3],
+    widths 64 / 128 / 256 / 512, a 1x1-conv + BatchNorm downsample on the first block of layers
+    2-4), without fc: the reference replaces fc and avgpool by empty Sequentials (encoder.py:66-67).
+    Restated from torchvision's published architecture (torchvision is absent offline)."""
+    keys = {"conv1.weight": (64, 3, 7, 7)}
+
+    def bn(prefix, c):
+        for n in ("weight", "bias", "running_mean", "running_var"):
+            keys["%s.%s" % (prefix, n)] = (c,)
+        keys[prefix + ".num_batches_tracked"] = ()
+
+    bn("bn1", 64)
+    cin = 64
+    for li, (blocks, c) in enumerate(zip((3, 4, 6, 3), (64, 128, 256, 512)), 1):
+        for b in range(blocks):
+            p = "layer%d.%d" % (li, b)
+            keys[p + ".conv1.weight"] = (c, cin if b == 0 else c, 3, 3)
+            bn(p + ".bn1", c)
+            keys[p + ".conv2.weight"] = (c, c, 3, 3)
+            bn(p + ".bn2", c)
+            if b == 0 and li > 1:
+                keys[p + ".downsample.0.weight"] = (c, cin, 1, 1)
+                bn(p + ".downsample.1", c)
+        cin = c
+    return keys
+
+
+def test_encoder_state_dict_matches_torchvision_resnet34_names_and_shapes():
+    """A reference checkpoint's ``encoder.model.*`` entries load by name and shape (models.py:268-298,
+    strict): every key of the in-repo trunk is torchvision ResNet-34's, with its shape, in its order."""
+    from pnr.encoder import SpatialEncoder
+
+    got = {k: tuple(v.shape) for k, v in SpatialEncoder(pretrained=False).model.state_dict().items()}
+    exp = _torchvision_resnet34_keys()
+    assert list(got) == list(exp)
+    assert got == exp
+    net_keys = [k for k in PixelNeRFNet(_conf_dict()).state_dict() if k.startswith("encoder.")]
+    assert net_keys == ["encoder.model." + k for k in exp]
+
+
+def _encoder_fixture():
+    import json
+    import os
+
+    g = dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "encoder_fw.npz")))
+    return g, json.loads(bytes(g["cases"]).decode())
+
+
+def test_encoder_forward_matches_reference_fixture_cpu():
+    """The module path of pnr.encoder.SpatialEncoder.forward on the CPU against the reference's own
+    SpatialEncoder.forward (encoder.py:111-164; tests/golden/make_encoder_golden.py): feature_scale,
+    use_first_pool, num_layers 3 / 4, the align_corners upsample + concat and latent_scaling, in eval
+    mode and in train mode (batch statistics, and the running-statistics update)."""
+    from pnr.encoder import SpatialEncoder
+
+    g, cases = _encoder_fixture()
+    imgs = torch.from_numpy(g["images"])
+    for i, c in enumerate(cases):
+        enc = SpatialEncoder(pretrained=False, num_layers=c["num_layers"], feature_scale=c["feature_scale"],
+                             use_first_pool=c["use_first_pool"])
+        enc.model.load_state_dict(synth.encoder_state(int(g["weight_seed"]), enc.model.state_dict()))
+        enc.train(c["train"])
+        with torch.no_grad():
+            lat = enc(imgs if c["train"] else imgs[:1])
+        ref = torch.from_numpy(g["latent_%d" % i])
+        assert lat.shape == ref.shape, (c, lat.shape)
+        scale = float(ref.abs().max())
+        # eval: 1e-6 of the latent's range (measured 2e-7); train: batch statistics over 2 x 12 x 12
+        # values amplify the convolutions' fp32 reordering (channels-last here) to ~1.2e-5
+        tol = 3e-5 if c["train"] else 1e-6
+        assert float((lat - ref).abs().max()) <= tol * scale + 1e-7, (c, float((lat - ref).abs().max()), scale)
+        torch.testing.assert_close(enc.latent_scaling, torch.from_numpy(g["latent_scaling_%d" % i]))
+        if c["train"]:
+            torch.testing.assert_close(enc.model.bn1.running_mean, torch.from_numpy(g["running_mean_after_%d" % i]))
