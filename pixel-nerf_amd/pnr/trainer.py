@@ -39,11 +39,14 @@ def _mse(a, b):
 
 
 def calc_losses(net, render_par, data, *, device, z_near, z_far, nviews=(1,), ray_batch_size=128,
-                use_bbox=False, lambda_coarse=1.0, lambda_fine=1.0, is_train=True):
+                use_bbox=False, lambda_coarse=1.0, lambda_fine=1.0, is_train=True, nviews_gen=None):
     """One batch's losses (train.py:193-283).  ``data`` is a collated SRN batch: images
     (SB, NV, 3, H, W) in [-1, 1], poses (SB, NV, 4, 4), focal (SB) or (SB, 2), optional c
     (SB, 2) and bbox (SB, NV, 4).  Returns {"rc", "rf" (if fine), "t"} as floats; with
-    ``is_train`` the loss is back-propagated first."""
+    ``is_train`` the loss is back-propagated first.  ``nviews_gen``: the torch.Generator the
+    batch's view count is drawn from (None: torch's default generator, as train.py:214 does); the
+    Trainer passes one seeded identically on every rank, so all ranks encode the same NS in a step,
+    as the reference's single process does for the whole SB batch."""
     if "images" not in data:
         return {}
     images = data["images"].to(device=device)
@@ -54,7 +57,7 @@ def calc_losses(net, render_par, data, *, device, z_near, z_far, nviews=(1,), ra
     cs = data.get("c")
 
     # views per object this batch: one of ``nviews`` (train.py:214-218)
-    cur = nviews[torch.randint(0, len(nviews), ()).item()]
+    cur = nviews[torch.randint(0, len(nviews), (), generator=nviews_gen).item()]
     order = torch.randint(0, NV, (SB, 1)) if cur == 1 else torch.empty((SB, cur), dtype=torch.long)
     rgb_gt, rays = [], []
     for o in range(SB):
@@ -147,10 +150,13 @@ class Trainer:
             self.use_bbox = False
             self.log(">>> Stopped using bbox sampling @ iter %d" % step)
         c = self.conf
+        gen = None
+        if self.world > 1:   # the same view count on every rank
+            gen = torch.Generator().manual_seed(getattr(self.args, "seed", 0) * 1000003 + 2 * step + int(not is_train))
         return calc_losses(self.net, self.render_par, data, device=self.device, z_near=self.z_near, z_far=self.z_far,
                            nviews=self.args.nviews, ray_batch_size=self.args.ray_batch_size,
                            use_bbox=self.use_bbox, lambda_coarse=c.get("lambda_coarse", 1.0),
-                           lambda_fine=c.get("lambda_fine", 1.0), is_train=is_train)
+                           lambda_fine=c.get("lambda_fine", 1.0), is_train=is_train, nviews_gen=gen)
 
     def save(self, step):
         if self.rank != 0:
@@ -171,7 +177,11 @@ class Trainer:
         accu = c.get("accu_grad", 1)
         val_iter = iter(self.val_loader) if self.val_loader is not None else None
         last = {}
-        self.net.train()
+        # train.py builds render_par with .eval() (train.py:93): step 0 runs with the net and the
+        # renderer in eval mode (BatchNorm on running statistics, no sigma noise); trainlib's
+        # batch-0 eval step then switches them to train (trainer.py:185-189)
+        self.net.eval()
+        self.renderer.eval()
         self.optim.zero_grad(set_to_none=True)
         for epoch in range(a.epochs):
             if self.sampler is not None:
@@ -197,6 +207,9 @@ class Trainer:
                     self.net.train()
                     if self.rank == 0:
                         self.log("*** Eval: E %d B %d %s" % (epoch, batch, " ".join("%s:%.6f" % kv for kv in vl.items())))
+                elif val_iter is None and not self.net.training:
+                    self.renderer.train()   # no eval split: train mode from the second step
+                    self.net.train()
                 if batch % c.get("save_interval", 50) == 0 and (epoch > 0 or batch > 0):
                     self.save(step)
                 if batch == batches - 1 or batch % accu == accu - 1:

@@ -170,8 +170,8 @@ def test_train_script_end_to_end_and_resume(tmp_path):
     write_srn_dir(str(tmp_path), make_inputs(n_obj=1, n_views=3, size=24, seed=5), stage="test")
     (tmp_path / "train.conf").write_text(TRAIN_CONF)
     common = [sys.executable, os.path.join(REPO, "scripts", "train.py"), "-c", str(tmp_path / "train.conf"),
-              "-D", root, "-n", "synth", "--checkpoints_path", str(tmp_path / "ck"), "-B", "2", "-V", "1",
-              "-R", "64", "--image_size", "24"]
+              "-D", root, "-F", "srn", "-n", "synth", "--checkpoints_path", str(tmp_path / "ck"),
+              "--visual_path", str(tmp_path / "vis"), "-B", "2", "-V", "1", "-R", "64", "--image_size", "24"]
     r = subprocess.run(common + ["--max_steps", "3"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     assert "final losses" in r.stdout and "*** Eval" in r.stdout, r.stdout[-2000:]
@@ -186,7 +186,7 @@ def test_train_script_end_to_end_and_resume(tmp_path):
     assert vals and all(np.isfinite(vals))
     r2 = subprocess.run(common + ["--resume", "--max_steps", "2"], capture_output=True, text=True, timeout=300)
     assert r2.returncode == 0, r2.stderr[-3000:]
-    assert "Load" in r2.stdout
+    assert "Load" in r2.stdout and "CONTINUE? yes" in r2.stdout
     assert torch.load(str(ck / "_iter"), weights_only=True)["iter"] == 5
 
 
@@ -200,9 +200,11 @@ class _TinyNet(torch.nn.Module):
         self.encoder = torch.nn.Sequential(torch.nn.BatchNorm2d(3))
         self.w = torch.nn.Parameter(torch.full((3,), 0.5))
         self.col = None
+        self.log = []
 
     def encode(self, images, poses, focal, c=None):
         self.col = images.mean(dim=(0, 1, 3, 4))
+        self.log.append((int(images.shape[1]), bool(self.training)))   # (NS, train mode) per encode
 
     def load_weights(self, args, opt_init=False, strict=True, device=None):
         path = os.path.join(args.checkpoints_path, args.name, "pixel_nerf_latest")
@@ -248,12 +250,12 @@ class _Objects(torch.utils.data.Dataset):
         return self.items[i]
 
 
-def _trainer_args(ck, resume=False):
+def _trainer_args(ck, resume=False, nviews=(1,)):
     import types
 
     return types.SimpleNamespace(checkpoints_path=ck, name="tiny", resume=resume, batch_size=2, lr=0.05,
-                                 gamma=1.0, gamma_delay=0, epochs=1, ray_batch_size=16, nviews=[1],
-                                 no_bbox_step=100)
+                                 gamma=1.0, gamma_delay=0, epochs=2, ray_batch_size=16, nviews=list(nviews),
+                                 no_bbox_step=100, seed=0)
 
 
 def _trainer_worker(rank, world, port, ck, q):
@@ -265,13 +267,14 @@ def _trainer_worker(rank, world, port, ck, q):
     pdist.init_from_env("gloo")
     trainer.seed_everything(rank)
     net = _TinyNet()
-    t = trainer.Trainer(net, _TinyRenderer(), _Objects(), None, _trainer_args(ck), {"print_interval": 100,
-                        "save_interval": 100}, torch.device("cpu"), log=lambda *_: None)
+    t = trainer.Trainer(net, _TinyRenderer(), _Objects(), None, _trainer_args(ck, nviews=(1, 2, 3)),
+                        {"print_interval": 100, "save_interval": 100}, torch.device("cpu"), log=lambda *_: None)
+    t.sampler.set_epoch(0)
     seen = [int(o) for d in t.loader for o in d["obj"]]
     last = t.start()
     # plain Python values: a tensor put on the queue is shared through a handle that dies with
     # this process
-    q.put((rank, seen, net.w.detach().tolist(), type(net.encoder[0]).__name__, dict(last)))
+    q.put((rank, seen, net.w.detach().tolist(), type(net.encoder[0]).__name__, dict(last), net.log))
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()
 
@@ -296,13 +299,18 @@ def test_trainer_two_rank_gloo(tmp_path):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, seen0, w0, bn0, l0), (r1, seen1, w1, bn1, l1) = res
+    (r0, seen0, w0, bn0, l0, log0), (r1, seen1, w1, bn1, l1, log1) = res
     assert sorted(seen0 + seen1) == list(range(8)) and not set(seen0) & set(seen1)
+    # -V "1 2 3": every step's view count is the same on both ranks (one draw per step for the whole
+    # batch, as the reference's single process), and it varies over the steps; step 0 runs in eval
+    # mode (train.py:93's render_par.eval()), the later steps in train mode
+    assert [n for n, _ in log0] == [n for n, _ in log1] and len({n for n, _ in log0}) > 1, (log0, log1)
+    assert [m for _, m in log0] == [False] + [True] * (len(log0) - 1)
     w0, w1 = torch.tensor(w0), torch.tensor(w1)
     assert torch.equal(w0, w1) and not torch.equal(w0, torch.full((3,), 0.5))
     assert bn0 == bn1 == "SyncBatchNorm2d"
     assert np.isfinite(l0["t"]) and np.isfinite(l1["t"])
-    assert torch.load(os.path.join(ck, "tiny", "_iter"), weights_only=True)["iter"] == 2
+    assert torch.load(os.path.join(ck, "tiny", "_iter"), weights_only=True)["iter"] == 4   # 2 epochs x 2
     assert torch.equal(torch.load(os.path.join(ck, "tiny", "pixel_nerf_latest"), weights_only=True)["w"], w0)
 
 
@@ -327,8 +335,9 @@ def test_train_script_two_ranks(tmp_path):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "scripts", "train.py"),
-           "-c", str(tmp_path / "train.conf"), "-D", root, "-n", "synth2", "--checkpoints_path", str(tmp_path / "ck"),
-           "-B", "1", "-V", "1", "-R", "32", "--image_size", "24", "--max_steps", "2"]
+           "-c", str(tmp_path / "train.conf"), "-D", root, "-F", "srn", "-n", "synth2", "--checkpoints_path",
+           str(tmp_path / "ck"), "--visual_path", str(tmp_path / "vis"), "-B", "1", "-V", "1", "-R", "32",
+           "--image_size", "24", "--max_steps", "2"]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert r.stdout.count("final losses") == 1, r.stdout[-2000:]
