@@ -439,8 +439,10 @@ class RenderPoints(torch.autograd.Function):
             side = None
             if DEFER_WGRAD and z.is_cuda and any(_defer_mask(ctx)):
                 side = _side_stream(z.device)
-            g, d_feat, d_zlat, deferred = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns,
-                                                             getattr(net, "wgrad_arith", "f16x3"), side)
+            res = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns,
+                                     getattr(net, "wgrad_arith", "f16x3"), side)
+            g, d_feat, d_zlat = res[:3]
+            deferred = res[3] if side is not None else None
         else:
             g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns, use_wgrad=net.mlp_precision == "f16x3")
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
