@@ -351,9 +351,6 @@ __device__ __forceinline__ int opaque_lane(int lane) {
     return lane;
 }
 
-#ifndef PNR_SAVE_NT
-#define PNR_SAVE_NT 0
-#endif
 // relu(acc) of this wave's rows -> save slot [point][512] (points of this tile < n_points)
 __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
@@ -366,12 +363,7 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
-#if PNR_SAVE_NT
-            // streaming store: the save is read once, by the backward kernels, long after
-            __builtin_nontemporal_store(relu4(v), reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g));
-#else
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = relu4(v);
-#endif
         }
     }
 }
@@ -1749,11 +1741,7 @@ __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t 
         if (p >= n_points) continue;
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
-#if PNR_SAVE_NT
-            __builtin_nontemporal_store(acc[r][c], reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g));
-#else
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = acc[r][c];
-#endif
     }
     if (bs) {   // bias gradient: this tile's column sums of the wave's rows, added to bs
         f4 sr[RTW];
@@ -1949,11 +1937,6 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
 #pragma unroll
                         for (int r = 0; r < RTW; ++r) {
                             f4 *q = reinterpret_cast<f4 *>(a.dzlat + (row0 + p) * H + 16 * (RTW * wave + r) + 4 * gz);
-#if PNR_SAVE_NT
-                            if (b == 0)   // the last update: read once by the input-stage backward
-                                __builtin_nontemporal_store(zfirst ? h[r][c] : *q + h[r][c], q);
-                            else
-#endif
                             *q = zfirst ? h[r][c] : *q + h[r][c];
                         }
                     }

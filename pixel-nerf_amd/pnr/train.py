@@ -29,8 +29,6 @@ util.py:461-471) and the input-stage backward scatters into each view's latent. 
 f16x3 backward chain (``pnr_mlp_backward_views``) covers any number of views; the fp32 / bf16
 arithmetics run the ResnetFC backward as per-layer GEMMs (``mlp_backward``).
 """
-import os
-
 import torch
 
 from . import _lib, ops
@@ -225,21 +223,14 @@ def _tall_mm(a, b):
     return (a.view(s, P // s, a.shape[1]).transpose(1, 2) @ b.view(s, P // s, b.shape[1])).sum(0)
 
 
-def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1, wgrad_arith="f16x3", wgrad_stream=None):
+def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1, wgrad_arith="f16x3"):
     """``mlp_backward`` for f16x3 models: the input-gradient chain (masks, residual adds,
     every 512-wide W^T GEMM, the summed latent gradient, the view mean's backward for ``ns``
     source views) runs in one ``pnr_mlp_backward_views`` launch on the forward's split-fp16
     GEMM, which also sums every layer's output gradient over its rows (the bias gradients,
     without re-reading dy); the 512-wide weight gradients are ``pnr_weight_grad`` launches
     (fp16 split products, fp32-level), one per row count (ns P view rows before combine_layer, P
-    after), over its per-layer output gradients and the activation save.
-
-    ``wgrad_stream``: None, or a stream the weight gradients (the 512-wide ones, lin_out's and
-    lin_in's) are launched on, after the chain, so they run beside whatever the caller launches
-    next on the current stream (the latent / encoder backward).  Returns ({param: grad},
-    d_feat, d_zlat, deferred) with ``deferred`` None, or (event recorded on ``wgrad_stream``
-    after the last weight-gradient launch, {param: grad}): those grads are valid on a stream
-    only after it waits on the event."""
+    after), over its per-layer output gradients and the activation save."""
     desc, packed, packed_t = mlp.packed_t(code, precision)
     nb = mlp.n_blocks
     nc = min(mlp.combine_layer, nb) if ns > 1 else nb
@@ -263,128 +254,37 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1, wgrad_arith="f1
                "pnr_mlp_backward_views")
     _ev_end("mlp_backward", e0, backward_chain_flop(mlp, P, ns))
     g = {}
+    xf = slot(2 * nb, P)
+    g[mlp.lin_out.weight] = _tall_mm(d_o, xf)
+    g[mlp.lin_out.bias] = d_o.sum(0)
+    # weight gradients grouped by row count: fc_0 (dY^T relu(x_b)), fc_1 (dY^T relu(h_b)),
+    # lin_z (dY^T z)
+    jobs = {}
+    for b, blk in enumerate(mlp.blocks):
+        rows = R if b < nc else P
+        jobs.setdefault(rows, []).extend([(blk.fc_0.weight, dy[b, :rows], slot(b, rows)),
+                                          (blk.fc_1.weight, dy[nb + 1 + b, :rows], slot(nb + b, rows))])
+    for b, lz in enumerate(lin_z):
+        rows = R if b < nc else P
+        jobs.setdefault(rows, []).append((lz.weight, dy[nb + b, :rows], z[:rows]))
+    for rows, js in jobs.items():
+        for i in range(0, len(js), 16):   # pnr_weight_grad: up to 16 layers per launch
+            part = js[i:i + 16]
+            gw = weight_grad([d for _, d, _ in part], [x for _, _, x in part], rows, wgrad_arith)
+            for j, (param, _, _) in enumerate(part):
+                g[param] = gw[j]
     for b, blk in enumerate(mlp.blocks):
         g[blk.fc_0.bias] = sums[b]
         g[blk.fc_1.bias] = sums[nb + 1 + b]
     for b, lz in enumerate(lin_z):
         g[lz.bias] = sums[nb + b]
-    g[mlp.lin_in.bias] = sums[nb]
-    g[mlp.lin_out.bias] = d_o.sum(0)
     dx = dy[nb]
     d_in = mlp.lin_in.weight.shape[1]
-
-    def weight_grads():
-        """dY^T X of every weight (fc_0: relu(x_b), fc_1: relu(h_b), lin_z: z, lin_out: x_f,
-        lin_in: the features), grouped by row count."""
-        gw_all = {mlp.lin_out.weight: _tall_mm(d_o, slot(2 * nb, P)),
-                  mlp.lin_in.weight: _tall_mm(dx, feat)[:, :d_in].contiguous()}
-        jobs = {}
-        for b, blk in enumerate(mlp.blocks):
-            rows = R if b < nc else P
-            jobs.setdefault(rows, []).extend([(blk.fc_0.weight, dy[b, :rows], slot(b, rows)),
-                                              (blk.fc_1.weight, dy[nb + 1 + b, :rows], slot(nb + b, rows))])
-        for b, lz in enumerate(lin_z):
-            rows = R if b < nc else P
-            jobs.setdefault(rows, []).append((lz.weight, dy[nb + b, :rows], z[:rows]))
-        for rows, js in jobs.items():
-            for i in range(0, len(js), 16):   # pnr_weight_grad: up to 16 layers per launch
-                part = js[i:i + 16]
-                gw = weight_grad([d for _, d, _ in part], [x for _, _, x in part], rows, wgrad_arith)
-                for j, (param, _, _) in enumerate(part):
-                    gw_all[param] = gw[j]
-        return gw_all
-
-    deferred = None
-    if wgrad_stream is None:
-        g.update(weight_grads())
-    else:
-        # the side stream starts after the chain; the tensors it reads were allocated on the
-        # current stream, so the allocator must not hand their blocks out again before it is done
-        wgrad_stream.wait_stream(torch.cuda.current_stream(dev))
-        for t in (save, dy, d_o):
-            t.record_stream(wgrad_stream)
-        with torch.cuda.stream(wgrad_stream):
-            gd = weight_grads()
-            done = torch.cuda.Event()
-            done.record(wgrad_stream)
-        deferred = (done, gd)
+    g[mlp.lin_in.weight] = _tall_mm(dx, feat)[:, :d_in]
+    g[mlp.lin_in.bias] = sums[nb]
     d_feat = torch.zeros(R, 64, device=dev, dtype=torch.float32)
     d_feat[:, :d_in] = dx @ mlp.lin_in.weight.detach()
-    if wgrad_stream is None:
-        return g, d_feat, dzl
-    return g, d_feat, dzl, deferred
-
-
-# ---- weight gradients beside the rest of the backward -------------------------------------------
-# RenderPoints.backward launches the 512-wide weight gradients of its MLP on a side stream (one per
-# device) and hands them to the parameters at the end of the backward pass (an engine callback:
-# the launch stream waits on the side stream's event, then .grad is set or accumulated and the
-# parameter's post-accumulate-grad hooks run, as AccumulateGrad would).  So k_wgrad_h runs beside
-# the latent / encoder backward, whose small MIOpen and elementwise launches leave most of the
-# chip idle.  The engine still runs a deferred parameter's post-accumulate-grad hooks when its
-# AccumulateGrad node executes, with .grad None; they run again once the gradient is set
-# (pnr.dist.GradReducer ignores the first call).
-# Only parameters whose AccumulateGrad node this backward pass executes are deferred
-# (leaf parameters under loss.backward()); torch.autograd.grad(..., inputs=params) and
-# nn.DataParallel replicas (non-leaf parameters) get their gradients through autograd as before.
-DEFER_WGRAD = os.environ.get("PNR_DEFER_WGRAD", "0") == "1"   # A/B knob; off: in order
-# PNR_WGRAD_CUMASK: the side stream restricted to a CU subset (hipExtStreamCreateWithCUMask), so the
-# weight gradients leave CUs to the encoder backward instead of competing for all of them:
-# "N" = the first N mask bits, "xS" = every CU except each S-th bit (a hex string "0x..." = the mask)
-WGRAD_CUMASK = os.environ.get("PNR_WGRAD_CUMASK", "")
-_SIDE = {}
-
-
-def _cumask_words(spec, n_cu):
-    if spec.startswith("0x"):
-        v = int(spec, 16)
-        bits = [(v >> i) & 1 for i in range(n_cu)]
-    elif spec.startswith("x"):
-        step = int(spec[1:])
-        bits = [0 if i % step == step - 1 else 1 for i in range(n_cu)]
-    else:
-        n = int(spec)
-        bits = [1 if i < n else 0 for i in range(n_cu)]
-    words = [0] * ((n_cu + 31) // 32)
-    for i, b in enumerate(bits):
-        words[i // 32] |= b << (i % 32)
-    return words
-
-
-def _side_stream(dev):
-    s = _SIDE.get(dev.index)
-    if s is None:
-        if WGRAD_CUMASK:
-            import ctypes
-
-            hip = ctypes.CDLL("libamdhip64.so.7")
-            n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
-            words = _cumask_words(WGRAD_CUMASK, n_cu)
-            arr = (ctypes.c_uint32 * len(words))(*words)
-            h = ctypes.c_void_p()
-            with torch.cuda.device(dev):
-                rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(len(words)), arr)
-            if rc != 0:
-                raise RuntimeError("hipExtStreamCreateWithCUMask failed (%d)" % rc)
-            s = torch.cuda.ExternalStream(h.value, device=dev)
-        else:
-            s = torch.cuda.Stream(dev)
-        _SIDE[dev.index] = s
-    return s
-
-
-def _deliver(stream, done, items):
-    """Engine callback: the deferred weight gradients become the parameters' .grad on ``stream``."""
-    stream.wait_event(done)
-    with torch.cuda.stream(stream):
-        for p, gr in items:
-            gr.record_stream(stream)   # allocated on the side stream, used here and by the optimizer
-            if p.grad is None:
-                p.grad = gr
-            else:
-                p.grad.add_(gr)
-            for hook in (getattr(p, "_post_accumulate_grad_hooks", None) or {}).values():
-                hook(p)
+    return g, d_feat, dzl
 
 
 class RenderPoints(torch.autograd.Function):
@@ -434,15 +334,9 @@ class RenderPoints(torch.autograd.Function):
         d_o = torch.cat([d_out[:, :3] * out[:, :3] * (1.0 - out[:, :3]),
                          d_out[:, 3:] * (out[:, 3:] > 0)], dim=1)
         ns = net.num_views_per_obj
-        deferred = None
         if net.mlp_precision == "f16x3":
-            side = None
-            if DEFER_WGRAD and z.is_cuda and any(_defer_mask(ctx)):
-                side = _side_stream(z.device)
-            res = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns,
-                                     getattr(net, "wgrad_arith", "f16x3"), side)
-            g, d_feat, d_zlat = res[:3]
-            deferred = res[3] if side is not None else None
+            g, d_feat, d_zlat = mlp_backward_fused(mlp, net.code, net.mlp_precision, save, d_o, P, ns,
+                                                   getattr(net, "wgrad_arith", "f16x3"))
         else:
             g, d_feat, d_zlat = mlp_backward(mlp, save, d_o, P, ns, use_wgrad=net.mlp_precision == "f16x3")
         need_z, need_lat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
@@ -461,37 +355,7 @@ class RenderPoints(torch.autograd.Function):
                                                      _lib.ptr(d_z), _lib.stream_of(z.device)),
                        "pnr_points_input_backward")
         grads = [g.get(p) for p in ctx.params]
-        if deferred is not None:
-            done, gd = deferred
-            mask = _defer_mask(ctx)
-            items = []
-            for i, p in enumerate(ctx.params):
-                if p in gd:
-                    if mask[i]:
-                        items.append((p, gd[p]))
-                    else:   # through autograd: valid on this stream after the side stream's event
-                        torch.cuda.current_stream(z.device).wait_event(done)
-                        grads[i] = gd[p]
-            if items:
-                stream = torch.cuda.current_stream(z.device)
-                torch.autograd.Variable._execution_engine.queue_callback(lambda: _deliver(stream, done, items))
         return (None, None, None, d_z.view(B, K) if need_z else None, d_lat, *grads)
-
-
-def _defer_mask(ctx):
-    """Per MLP parameter of RenderPoints: is its gradient accumulated by a leaf AccumulateGrad
-    node that this backward pass executes (so it may be handed over at the end of the pass)?"""
-    out = []
-    nf = ctx.next_functions   # one entry per tensor input: rays, z, latent_cl, *params
-    for node, _ in nf[len(nf) - len(ctx.params):]:
-        ok = node is not None and type(node).__name__ == "AccumulateGrad"
-        if ok:
-            try:
-                ok = torch._C._will_engine_execute_node(node)
-            except RuntimeError:   # torch.autograd.grad(): leaf nodes are not executed
-                ok = False
-        out.append(ok)
-    return out
 
 
 class Composite(torch.autograd.Function):

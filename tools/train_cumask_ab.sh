@@ -1,5 +1,6 @@
 #!/bin/bash
-# Training-step A/B (one box, alternating rounds, scripts/bench_train.py 20 steps):
+# Training-step A/B (one box, alternating rounds, scripts/bench_train.py 20 steps); the variants need
+# tools/patches/defer_wgrad_cumask.diff / save_nt.diff applied (rejected in round 5, profiles/r5b):
 #   base    the weight gradients in order on the launch stream
 #   defer   k_wgrad_h on a side stream beside the encoder backward (pnr.train DEFER_WGRAD)
 #   m<N>    defer, the side stream on the first N CUs (PNR_WGRAD_CUMASK=N, hipExtStreamCreateWithCUMask)
