@@ -116,6 +116,54 @@ __global__ __launch_bounds__(256) void k_composite_s(
     }
 }
 
+#ifndef PNR_COMP_PERSIST
+#define PNR_COMP_PERSIST 0   // A/B knob: waves stride over rays with the next ray's loads in flight
+#endif
+// Persistent form of k_composite_s: each wave strides over rays (wave g takes rays g, g + G, ...),
+// issuing ray i + 1's loads before compositing ray i, so every wave keeps a ray's bytes in flight
+// for its whole life instead of waiting on each ray's loads once per launch slot.
+template <int S>
+__global__ __launch_bounds__(256) void k_composite_p(
+    const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
+    int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
+    float *__restrict__ rgb_out, float *__restrict__ depth_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t stride = (int64_t)gridDim.x * 4;
+    int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= n_rays) return;
+    const int k0 = S * lane;
+    float zk[S], far;
+    f4 v[S];
+    auto load = [&](int64_t bb, float (&zz)[S], f4 (&vv)[S], float &ff) {
+        ff = rays[bb * 8 + 7];
+        const float *zr = z + bb * K;
+        const f4 *rr = reinterpret_cast<const f4 *>(raw) + bb * K;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const int kc = k0 + i < K ? k0 + i : K - 1;
+            zz[i] = __builtin_nontemporal_load(zr + kc);
+            vv[i] = __builtin_nontemporal_load(rr + kc);
+        }
+    };
+    load(b, zk, v, far);
+    for (;;) {
+        const int64_t bn = b + stride;
+        float zn[S], farn = 0.f;
+        f4 vn[S];
+        if (bn < n_rays) load(bn, zn, vn, farn);   // wave-uniform
+        float wk[S];
+        composite_wave<S>(lane, b, K, far, zk, v, white_bkgd, weights, rgb_out, depth_out, wk);
+        if (bn >= n_rays) break;
+        b = bn;
+        far = farn;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            zk[i] = zn[i];
+            v[i] = vn[i];
+        }
+    }
+}
+
 // any K: 64-sample chunks, one wave scan per chunk with a running carry
 __global__ __launch_bounds__(256) void k_composite(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
@@ -262,7 +310,16 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
     const int64_t blocks = (n_rays + per_block - 1) / per_block;
     auto kern = nch == 1 ? k_composite_s<1> : nch == 2 ? k_composite_s<2> : nch == 3 ? k_composite_s<3>
               : nch == 4 ? k_composite_s<4> : k_composite;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), 0, st, z, raw, rays,
+    int64_t grid = blocks;
+#if PNR_COMP_PERSIST
+    if (nch <= 4) {
+        kern = nch == 1 ? k_composite_p<1> : nch == 2 ? k_composite_p<2> : nch == 3 ? k_composite_p<3>
+             : k_composite_p<4>;
+        const int64_t cap = (int64_t)device_cu_count() * PNR_COMP_PERSIST;   // workgroups per CU
+        grid = (n_rays + 3) / 4 < cap ? (n_rays + 3) / 4 : cap;
+    }
+#endif
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, st, z, raw, rays,
                        n_rays, K, white_bkgd, weights, rgb, depth);
     return launch_ok("composite") ? PNR_OK : PNR_ERR_HIP;
 }
