@@ -116,6 +116,77 @@ __global__ __launch_bounds__(256) void k_composite_s(
     }
 }
 
+#ifndef PNR_COMP_CHUNKED
+#define PNR_COMP_CHUNKED 0   // A/B knob: lane l owns samples l, 64 + l, ... (one contiguous load per chunk)
+#endif
+// Chunked ownership: lane l holds samples 64 i + l (i < S), so each load instruction reads 1 KB
+// of raw (and 256 B of z) contiguously instead of every other 16 B of 2 KB; one exclusive double
+// product scan per 64-sample chunk with a running carry (the association of the generic
+// k_composite), then the same per-lane weight / colour sums.
+template <int S>
+__global__ __launch_bounds__(256) void k_composite_c(
+    const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
+    int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
+    float *__restrict__ rgb_out, float *__restrict__ depth_out) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= n_rays) return;
+    const float far = rays[b * 8 + 7];
+    const float *zr = z + b * K;
+    const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
+    float zk[S];
+    f4 v[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const int k = 64 * i + lane;
+        const int kc = k < K ? k : K - 1;
+        zk[i] = __builtin_nontemporal_load(zr + kc);
+        v[i] = __builtin_nontemporal_load(rr + kc);
+    }
+    double carry = 1.0;
+    float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+        const int k = 64 * i + lane;
+        const bool valid = k < K;
+        // the next sample's depth: lane + 1 of this chunk, or lane 0 of the next one for lane 63
+        const float nxt0 = i + 1 < S ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zk[i + 1 < S ? i + 1 : i]), 0))
+                                     : far;
+        const float zn = k + 1 >= K ? far : dpp_f<0x130>(nxt0, zk[i]);   // wave_shl:1
+        const float delta = sub_rn(zn, zk[i]);
+        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v[i].w, 0.0f)))) : 0.0f;
+        const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
+        const double incl = wave_scan_mul((double)shifted);
+        const double excl = wave_shr1(incl, 1.0);
+        const float wk = valid ? mul_rn(alpha, (float)(carry * excl)) : 0.f;
+        const long long il = __double_as_longlong(incl);
+        carry *= __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(il >> 32), 63) << 32) |
+                                      (unsigned)__builtin_amdgcn_readlane((int)il, 63));
+        if (weights && valid) __builtin_nontemporal_store(wk, weights + b * K + k);
+        sr += mul_rn(wk, v[i].x);
+        sg += mul_rn(wk, v[i].y);
+        sb += mul_rn(wk, v[i].z);
+        sd += mul_rn(wk, zk[i]);
+        sw += wk;
+    }
+    sr = wave_sum_dpp(sr);
+    sg = wave_sum_dpp(sg);
+    sb = wave_sum_dpp(sb);
+    sd = wave_sum_dpp(sd);
+    sw = wave_sum_dpp(sw);
+    if (lane == 0) {
+        if (white_bkgd) {
+            sr = sub_rn(add_rn(sr, 1.0f), sw);
+            sg = sub_rn(add_rn(sg, 1.0f), sw);
+            sb = sub_rn(add_rn(sb, 1.0f), sw);
+        }
+        rgb_out[b * 3 + 0] = sr;
+        rgb_out[b * 3 + 1] = sg;
+        rgb_out[b * 3 + 2] = sb;
+        depth_out[b] = sd;
+    }
+}
+
 #ifndef PNR_COMP_PERSIST
 #define PNR_COMP_PERSIST 0   // A/B knob: waves stride over rays with the next ray's loads in flight
 #endif
@@ -311,6 +382,10 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
     auto kern = nch == 1 ? k_composite_s<1> : nch == 2 ? k_composite_s<2> : nch == 3 ? k_composite_s<3>
               : nch == 4 ? k_composite_s<4> : k_composite;
     int64_t grid = blocks;
+#if PNR_COMP_CHUNKED
+    if (nch <= 4)
+        kern = nch == 1 ? k_composite_c<1> : nch == 2 ? k_composite_c<2> : nch == 3 ? k_composite_c<3> : k_composite_c<4>;
+#endif
 #if PNR_COMP_PERSIST
     if (nch <= 4) {
         kern = nch == 1 ? k_composite_p<1> : nch == 2 ? k_composite_p<2> : nch == 3 ? k_composite_p<3>
