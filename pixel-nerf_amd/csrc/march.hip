@@ -152,7 +152,10 @@ __global__ __launch_bounds__(256) void k_composite_c(
         // the next sample's depth: lane + 1 of this chunk, or lane 0 of the next one for lane 63
         const float nxt0 = i + 1 < S ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zk[i + 1 < S ? i + 1 : i]), 0))
                                      : far;
-        const float zn = k + 1 >= K ? far : dpp_f<0x130>(nxt0, zk[i]);   // wave_shl:1
+        // wave_shl:1, evaluated by every lane: under the select's branch the lane before the last
+        // valid one would read a disabled lane and keep `old`
+        const float zl = dpp_f<0x130>(nxt0, zk[i]);
+        const float zn = k + 1 >= K ? far : zl;
         const float delta = sub_rn(zn, zk[i]);
         const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v[i].w, 0.0f)))) : 0.0f;
         const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
