@@ -234,21 +234,25 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
                 // channel half * 256 + q * 64 + lane (q = vector element): coalesced 256-B rows
                 // per load, and the same lane-contiguous layout for the flush atomics
                 const int ch = half * 256 + lane;
-                f4 gv, l00, l01, l10, l11;
+                f4 gv;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    gv[q] = gz[ch + q * 64];
-                    l00[q] = latent[G.o00 + ch + q * 64];
-                    l01[q] = latent[G.o01 + ch + q * 64];
-                    l10[q] = latent[G.o10 + ch + q * 64];
-                    l11[q] = latent[G.o11 + ch + q * 64];
-                }
-                if (!G.inx1) { l01 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l01; }
-                if (!G.iny1) { l10 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l10; }
+                for (int q = 0; q < 4; ++q) gv[q] = gz[ch + q * 64];
+                if (d_z) {   // the latent corners only feed d ix / d iy (the depth chain)
+                    f4 l00, l01, l10, l11;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    dwe += gv[q] * ((1.f - wn) * (l01[q] - l00[q]) + wn * (l11[q] - l10[q]));
-                    dwn += gv[q] * ((1.f - we) * (l10[q] - l00[q]) + we * (l11[q] - l01[q]));
+                    for (int q = 0; q < 4; ++q) {
+                        l00[q] = latent[G.o00 + ch + q * 64];
+                        l01[q] = latent[G.o01 + ch + q * 64];
+                        l10[q] = latent[G.o10 + ch + q * 64];
+                        l11[q] = latent[G.o11 + ch + q * 64];
+                    }
+                    if (!G.inx1) { l01 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l01; }
+                    if (!G.iny1) { l10 = f4{0.f, 0.f, 0.f, 0.f}; l11 = l10; }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        dwe += gv[q] * ((1.f - wn) * (l01[q] - l00[q]) + wn * (l11[q] - l10[q]));
+                        dwn += gv[q] * ((1.f - we) * (l10[q] - l00[q]) + we * (l11[q] - l01[q]));
+                    }
                 }
                 acc[0][half] += wnw * gv;
                 acc[1][half] += wne * gv;

@@ -329,8 +329,9 @@ def _fused_bn_ok(bn, y, idt):
     c = y.shape[1] if y.dim() == 4 else 0
     return (FUSED_TRAIN_BN and type(bn) is nn.BatchNorm2d and bn.training and bn.affine and bn.momentum is not None
             and y.is_cuda and y.dtype == torch.float32 and c >= 4 and c % 4 == 0 and 256 % (c // 4) == 0
-            and y.numel() > 0 and _nhwc([y]) and bn.weight.dtype == torch.float32
-            and (idt is None or (idt.shape == y.shape and idt.dtype == y.dtype and _nhwc([idt]))))
+            and y.numel() > 0 and y.is_contiguous(memory_format=torch.channels_last) and bn.weight.dtype == torch.float32
+            and (idt is None or (idt.shape == y.shape and idt.dtype == y.dtype
+                                 and idt.is_contiguous(memory_format=torch.channels_last))))
 
 
 def bn_act(bn, y, relu=True, idt=None):
