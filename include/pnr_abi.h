@@ -33,7 +33,8 @@ extern "C" {
 #define PNR_ABI_VERSION 7   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
                                5: pnr_latent_channels_last_nhwc;
                                6: pnr_fold_batchnorm;
-                               7: pnr_batchnorm_train_forward / _backward */
+                               7: pnr_batchnorm_train_forward / _backward,
+                                  pnr_latent_channels_last_backward */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -320,6 +321,15 @@ int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *chann
                                   const int32_t *heights, const int32_t *widths, int32_t n_maps,
                                   int32_t n_images, float *latent_cl, int32_t out_h, int32_t out_w,
                                   pnr_stream_t stream);
+
+/* Backward of pnr_latent_channels_last_nhwc: d_maps[k] (n_images, heights[k], widths[k], channels[k],
+ * channels-last) = the adjoint of map k's bilinear upsample (align_corners = True) applied to its
+ * channel slice of g (n_images, out_h, out_w, sum channels) -- what autograd of encoder.py:150-160's
+ * F.interpolate + torch.cat computes (upsample_bilinear2d_backward).  Gathered per source element in
+ * a fixed order (deterministic; torch scatters with atomics); one launch for all maps (ABI 7). */
+int pnr_latent_channels_last_backward(const float *g, float *const *d_maps, const int32_t *channels,
+                                      const int32_t *heights, const int32_t *widths, int32_t n_maps,
+                                      int32_t n_images, int32_t out_h, int32_t out_w, pnr_stream_t stream);
 
 /* One (convolution, BatchNorm) pair of the eval-mode encoder trunk (encoder.py:135-149 with the
  * BatchNorms on their running statistics).  conv_w / w_out: n_out blocks of per_out contiguous

@@ -35,6 +35,8 @@ size_t wgrad_workspace_bytes(int, int64_t);
 int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
                  hipStream_t, int arith);
 int launch_fold_bn(const pnr_bn_fold *, int, int64_t, hipStream_t);
+int launch_latent_cl_bwd(const float *, float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, int,
+                         int, hipStream_t);
 size_t bn_workspace_bytes(int64_t, int);
 int launch_bn_forward(const float *, const float *, const float *, const float *, float *, float *, int64_t *, int64_t,
                       int, float, float, int, float *, float *, void *, size_t, hipStream_t);
@@ -605,6 +607,15 @@ int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *chann
         return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_nhwc: bad sizes");
     return launch_latent_cl(maps, channels, heights, widths, n_maps, n_images, latent_cl, out_h, out_w, true,
                             (hipStream_t)stream);
+}
+
+int pnr_latent_channels_last_backward(const float *g, float *const *d_maps, const int32_t *channels,
+                                      const int32_t *heights, const int32_t *widths, int32_t n_maps,
+                                      int32_t n_images, int32_t out_h, int32_t out_w, pnr_stream_t stream) {
+    if (!d_maps || !channels || !heights || !widths)
+        return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_backward: NULL");
+    return launch_latent_cl_bwd(g, d_maps, channels, heights, widths, n_maps, n_images, out_h, out_w,
+                                (hipStream_t)stream);
 }
 
 size_t pnr_batchnorm_workspace_bytes(int64_t M, int32_t C) { return M < 1 || C < 4 ? 0 : bn_workspace_bytes(M, C); }

@@ -65,6 +65,24 @@ class LatentChannelsLast(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if g.is_cuda and ctx.nhwc and g.dtype == torch.float32:
+            # channels-last maps (the trunk's layout): pnr_latent_channels_last_backward, one
+            # deterministic gather launch for every map
+            from . import _lib
+
+            g = g.contiguous()
+            n, h, w = g.shape[:3]
+            grads = [torch.empty(shp, dtype=torch.float32, device=g.device, memory_format=torch.channels_last)
+                     for shp in ctx.shapes]
+            k = len(grads)
+            ptrs = (ctypes.c_void_p * k)(*[t.data_ptr() for t in grads])
+            ch = (ctypes.c_int32 * k)(*[s[1] for s in ctx.shapes])
+            hs = (ctypes.c_int32 * k)(*[s[2] for s in ctx.shapes])
+            ws = (ctypes.c_int32 * k)(*[s[3] for s in ctx.shapes])
+            _lib.check(_lib.load().pnr_latent_channels_last_backward(
+                _lib.ptr(g), ptrs, ch, hs, ws, k, n, h, w, _lib.stream_of(g.device)),
+                "pnr_latent_channels_last_backward")
+            return tuple(grads)
         gn = g.permute(0, 3, 1, 2)   # NCHW view of the channels-last gradient
         h, w = gn.shape[-2:]
         grads, c0 = [], 0

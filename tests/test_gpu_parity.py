@@ -781,6 +781,35 @@ def test_latent_channels_last_backward_matches_torch_autograd(nhwc):
         assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item(), (a - b).abs().max().item()
 
 
+@pytest.mark.parametrize("out_hw,shapes", [
+    ((33, 47), [(3, 8, 33, 47), (3, 16, 17, 24), (3, 32, 9, 12), (3, 64, 5, 6)]),
+    ((64, 64), [(4, 64, 64, 64), (4, 64, 32, 32), (4, 128, 16, 16), (4, 256, 8, 8)]),   # cfg5's trunk
+    ((7, 9), [(2, 4, 7, 9), (2, 8, 1, 5), (2, 4, 3, 1), (2, 4, 2, 1)]),
+])
+def test_latent_backward_gather_matches_torch_and_is_deterministic(out_hw, shapes):
+    """pnr_latent_channels_last_backward (the adjoint gather for channels-last maps) against
+    torch's upsample_bilinear2d_backward on odd scales, 1-pixel maps and cfg5's trunk sizes;
+    bitwise repeatable (torch's scatter is atomic)."""
+    import torch.nn.functional as F
+
+    from pnr.encoder import LatentChannelsLast
+
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    maps = [torch.randn(sh, generator=gen).to(DEV).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            for sh in shapes]
+    out = LatentChannelsLast.apply(*maps)
+    ref = torch.cat([F.interpolate(m, out_hw, mode="bilinear", align_corners=True) for m in maps],
+                    1).permute(0, 2, 3, 1)
+    g = torch.randn(out.shape, generator=gen).to(DEV)
+    got = torch.autograd.grad(out, maps, g, retain_graph=True)
+    again = torch.autograd.grad(out, maps, g)
+    want = torch.autograd.grad(ref, maps, g)
+    for a, b, c in zip(got, want, again):
+        assert a.shape == b.shape and a.is_contiguous(memory_format=torch.channels_last)
+        assert (a - b).abs().max().item() <= 1e-5 * max(b.abs().max().item(), 1.0), (a - b).abs().max().item()
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("nhwc", [False, True])
 def test_latent_channels_last_matches_torch_upsample_concat(nhwc):
     """pnr_latent_channels_last (encoder.py:150-160 tail; NCHW maps) and
