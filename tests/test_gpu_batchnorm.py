@@ -5,7 +5,8 @@ The trunk's training-mode layers (encoder.py:135-149 over torchvision's BasicBlo
 output, running mean / variance (momentum, unbiased variance), num_batches_tracked, and the
 gradients of the map, the residual, gamma and beta.  Tolerance: fp32 rounding of the
 normalisation (torch reduces in fp32 Welford, the kernels in double): outputs within 2e-5 of
-their max-abs, gradients within 1e-4 of their max-abs, running statistics within 1e-5.
+their max-abs, gradients within 1e-4 of their max-abs (dy: of its terms' scale gamma invstd |dz|),
+running statistics within 1e-5.
 """
 import copy
 
@@ -58,7 +59,11 @@ def test_fused_batchnorm_matches_torch(shape, relu, add):
     dout = torch.randn(shape, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
     out.backward(dout)
     outr.backward(dout)
-    assert _rel(y.grad, yr.grad) < 1e-4
+    # dy is a difference of terms of size gamma invstd |dz|: measured against that scale (at M = 2
+    # the exact dy is 0 and both sides are rounding noise of it)
+    var = y0.double().var(dim=(0, 2, 3), unbiased=False)
+    term = ((bn.weight.double().abs() / (var + bn.eps).sqrt()).max() * dout.abs().max()).item()
+    assert (y.grad - yr.grad).abs().max().item() < 1e-4 * max(yr.grad.abs().max().item(), term)
     assert _rel(bn.weight.grad, ref.weight.grad) < 1e-4
     assert _rel(bn.bias.grad, ref.bias.grad) < 1e-4
     if add:
