@@ -66,63 +66,14 @@ __global__ __launch_bounds__(256) void k_merge_raw(const int *__restrict__ origi
 // One wave per ray, 4 rays per 256-thread block; the cumprod accumulates in double
 // (torch's CPU cumprod accumulates in double and rounds each prefix).
 // ---------------------------------------------------------------------------
-// S > 0 (K <= 64 S): lane l owns the S consecutive samples 64-lane-contiguous at S*l:
-// one sequential double product inside the lane, then ONE exclusive wave scan of the
-// lane products per ray; the next sample's z comes from the neighbour lane by shuffle.
-#ifndef PNR_COMP_RPW
-#define PNR_COMP_RPW 1   // rays per wave (A/B knob: 2 issues both rays' loads before the first scan)
-#endif
-template <int S>
-__global__ __launch_bounds__(256) void k_composite_s(
-    const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
-    int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
-    float *__restrict__ rgb_out, float *__restrict__ depth_out) {
-    constexpr int RPW = PNR_COMP_RPW;
-    const int lane = threadIdx.x & 63;
-    const int64_t b0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-    if (b0 >= n_rays) return;
-    const int k0 = S * lane;
-    float zk[RPW][S], far[RPW];
-    f4 v[RPW][S];
-    // unconditional (clamped) loads: every ray's loads issue before the first wait
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        const int64_t b = b0 + j < n_rays ? b0 + j : n_rays - 1;
-        far[j] = rays[b * 8 + 7];
-        const float *zr = z + b * K;
-        const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
-        if (S == 2 && (K & 1) == 0) {   // 8-B aligned pair of depths
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            const int kc = k0 < K ? k0 : K - 2;
-            const f2 zz = __builtin_nontemporal_load(reinterpret_cast<const f2 *>(zr + kc));
-            zk[j][0] = zz.x;
-            zk[j][S - 1] = zz.y;
-#pragma unroll
-            for (int i = 0; i < S; ++i) v[j][i] = __builtin_nontemporal_load(rr + kc + i);
-        } else {
-#pragma unroll
-            for (int i = 0; i < S; ++i) {
-                const int kc = k0 + i < K ? k0 + i : K - 1;
-                zk[j][i] = __builtin_nontemporal_load(zr + kc);
-                v[j][i] = __builtin_nontemporal_load(rr + kc);
-            }
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        if (b0 + j >= n_rays) break;
-        float wk[S];
-        composite_wave<S>(lane, b0 + j, K, far[j], zk[j], v[j], white_bkgd, weights, rgb_out, depth_out, wk);
-    }
-}
-
-#ifndef PNR_COMP_CHUNKED
-#define PNR_COMP_CHUNKED 0   // A/B knob: lane l owns samples l, 64 + l, ... (one contiguous load per chunk)
-#endif
-// Chunked ownership: lane l holds samples 64 i + l (i < S), so each load instruction reads 1 KB
-// of raw (and 256 B of z) contiguously instead of every other 16 B of 2 KB; one exclusive double
-// product scan per 64-sample chunk with a running carry (the association of the generic
-// k_composite), then the same per-lane weight / colour sums.
+// K <= 256 (S = ceil(K / 64) chunks): lane l holds samples 64 i + l (i < S), so each load
+// instruction reads 1 KB of raw (and 256 B of z) contiguously; all loads issue before the first
+// wait (clamped addresses).  One exclusive double product scan per 64-sample chunk (DPP
+// row_shr / row_bcast / wave_shr, no LDS) with a running carry -- the association of the generic
+// k_composite -- then per-lane weight / colour sums and DPP wave reductions.  Measured against the
+// lane-owns-S-consecutive-samples layout (k_composite_s, tools/patches/composite_variants.diff):
+// 0.435-0.453 ms against 0.508-0.516 ms per 1 M rays x 128 without weights, 0.543-0.548 against
+// 0.551-0.560 with them (profiles/r5h, same box, alternating).
 template <int S>
 __global__ __launch_bounds__(256) void k_composite_c(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
@@ -187,54 +138,6 @@ __global__ __launch_bounds__(256) void k_composite_c(
         rgb_out[b * 3 + 1] = sg;
         rgb_out[b * 3 + 2] = sb;
         depth_out[b] = sd;
-    }
-}
-
-#ifndef PNR_COMP_PERSIST
-#define PNR_COMP_PERSIST 0   // A/B knob: waves stride over rays with the next ray's loads in flight
-#endif
-// Persistent form of k_composite_s: each wave strides over rays (wave g takes rays g, g + G, ...),
-// issuing ray i + 1's loads before compositing ray i, so every wave keeps a ray's bytes in flight
-// for its whole life instead of waiting on each ray's loads once per launch slot.
-template <int S>
-__global__ __launch_bounds__(256) void k_composite_p(
-    const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
-    int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
-    float *__restrict__ rgb_out, float *__restrict__ depth_out) {
-    const int lane = threadIdx.x & 63;
-    const int64_t stride = (int64_t)gridDim.x * 4;
-    int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= n_rays) return;
-    const int k0 = S * lane;
-    float zk[S], far;
-    f4 v[S];
-    auto load = [&](int64_t bb, float (&zz)[S], f4 (&vv)[S], float &ff) {
-        ff = rays[bb * 8 + 7];
-        const float *zr = z + bb * K;
-        const f4 *rr = reinterpret_cast<const f4 *>(raw) + bb * K;
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-            const int kc = k0 + i < K ? k0 + i : K - 1;
-            zz[i] = __builtin_nontemporal_load(zr + kc);
-            vv[i] = __builtin_nontemporal_load(rr + kc);
-        }
-    };
-    load(b, zk, v, far);
-    for (;;) {
-        const int64_t bn = b + stride;
-        float zn[S], farn = 0.f;
-        f4 vn[S];
-        if (bn < n_rays) load(bn, zn, vn, farn);   // wave-uniform
-        float wk[S];
-        composite_wave<S>(lane, b, K, far, zk, v, white_bkgd, weights, rgb_out, depth_out, wk);
-        if (bn >= n_rays) break;
-        b = bn;
-        far = farn;
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-            zk[i] = zn[i];
-            v[i] = vn[i];
-        }
     }
 }
 
@@ -380,23 +283,9 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
                      int white_bkgd, float *weights, float *rgb, float *depth, hipStream_t st) {
     if (n_rays == 0) return PNR_OK;
     const int nch = (K + 63) / 64;
-    const int64_t per_block = 4 * (nch <= 4 ? PNR_COMP_RPW : 1);
-    const int64_t blocks = (n_rays + per_block - 1) / per_block;
-    auto kern = nch == 1 ? k_composite_s<1> : nch == 2 ? k_composite_s<2> : nch == 3 ? k_composite_s<3>
-              : nch == 4 ? k_composite_s<4> : k_composite;
-    int64_t grid = blocks;
-#if PNR_COMP_CHUNKED
-    if (nch <= 4)
-        kern = nch == 1 ? k_composite_c<1> : nch == 2 ? k_composite_c<2> : nch == 3 ? k_composite_c<3> : k_composite_c<4>;
-#endif
-#if PNR_COMP_PERSIST
-    if (nch <= 4) {
-        kern = nch == 1 ? k_composite_p<1> : nch == 2 ? k_composite_p<2> : nch == 3 ? k_composite_p<3>
-             : k_composite_p<4>;
-        const int64_t cap = (int64_t)device_cu_count() * PNR_COMP_PERSIST;   // workgroups per CU
-        grid = (n_rays + 3) / 4 < cap ? (n_rays + 3) / 4 : cap;
-    }
-#endif
+    const int64_t grid = (n_rays + 3) / 4;   // one wave per ray
+    auto kern = nch == 1 ? k_composite_c<1> : nch == 2 ? k_composite_c<2> : nch == 3 ? k_composite_c<3>
+              : nch == 4 ? k_composite_c<4> : k_composite;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, st, z, raw, rays,
                        n_rays, K, white_bkgd, weights, rgb, depth);
     return launch_ok("composite") ? PNR_OK : PNR_ERR_HIP;

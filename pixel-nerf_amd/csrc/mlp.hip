@@ -644,9 +644,44 @@ struct Fair {
     int *prog;   // LDS: iteration count per wave (8 ints)
     int wave, it, mate;
 };
-template <int NKS, int DIST = H_DIST>
+// Activation save drained from the LDS image during the GEMM that reads it (training forward,
+// PNR_SAVE_DRAIN): lane l of wave w owns column 8 w + (l >> 3) of the tile and, at k-step ks,
+// its 4 channels 32 ks + 4 (l & 7); the GEMM's k-step reads them from P0 / P1 beside its own B
+// fragments and stores (P0 + P1) 2^-e_col (the value the GEMM multiplies) as one 16-B store issued
+// after the k-step's last ring load, so the save streams out one store per lane per k-step
+// instead of the publish's 16-store burst whose completion the next ring waits queued behind
+// (vmcnt counts stores and loads in order).
+#ifndef PNR_SAVE_DRAIN
+#define PNR_SAVE_DRAIN 0
+#endif
+struct Drain {
+    float *base;            // save slot row of the tile's column 0 (uniform)
+    const _Float16 *p0;     // the image's P0 (P1 = p0 + PART_HALVES)
+    const int *ecol;        // the image's column exponents
+    int wave;               // (uniform)
+    int n_cols;             // columns of the tile that are points (uniform)
+};
+// this lane's part of k-step ks: everything recomputed from the lane id (no registers held
+// across the GEMM's k-steps, where the accumulators and the ring fill the register file)
+__device__ __forceinline__ void drain_step(const Drain &D, int ks) {
+    const int ln = (int)__lane_id(), j = ln & 7, col = 8 * D.wave + (ln >> 3);
+    if (col >= D.n_cols) return;
+    const _Float16 *src = D.p0 + col * ROWH + 32 * ks + 8 * ((j >> 1) ^ ((col >> 2) & 3)) + 4 * (j & 1);
+    const u2 q0 = *reinterpret_cast<const u2 *>(src);
+    const u2 q1 = *reinterpret_cast<const u2 *>(src + PART_HALVES);
+    const float inv = __builtin_ldexpf(1.f, -D.ecol[col]);
+    const f2 a0 = __builtin_convertvector(__builtin_bit_cast(h2, q0.x), f2);
+    const f2 a1 = __builtin_convertvector(__builtin_bit_cast(h2, q0.y), f2);
+    const f2 c0 = __builtin_convertvector(__builtin_bit_cast(h2, q1.x), f2);
+    const f2 c1 = __builtin_convertvector(__builtin_bit_cast(h2, q1.y), f2);
+    *reinterpret_cast<f4 *>(D.base + col * H + 32 * ks + 4 * j) =
+        f4{a0.x + c0.x, a0.y + c0.y, a1.x + c1.x, a1.y + c1.y} * inv;
+}
+
+template <int NKS, int DIST = H_DIST, bool DRAIN = false>
 __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const float *__restrict__ wp,
-                                                const _Float16 *pb0, const _Float16 *pb1, Fair *F = nullptr) {
+                                                const _Float16 *pb0, const _Float16 *pb1, Fair *F = nullptr,
+                                                const Drain *D = nullptr) {
     constexpr int H_RING = HRing<DIST>::slots;   // register ring slots
     static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
@@ -656,8 +691,13 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
     auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
         constexpr int ph = decltype(ph_tag)::value;
         constexpr bool tail = decltype(tail_tag)::value;
-        h8 b0[CT], b1[CT];
         const int kr = ks & (NKS - 1);
+        // the drain first: the previous k-step's B fragments are dead here (32 fewer live VGPRs)
+        if constexpr (DRAIN) {
+            drain_step(*D, kr);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        h8 b0[CT], b1[CT];
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             b0[c] = *reinterpret_cast<const h8 *>(pb0 + c * 16 * ROWH + 32 * kr);
@@ -993,7 +1033,7 @@ __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, 
 // that publish's registers (g.ecl) instead of LDS, so the accumulator scaling does not wait on a read.
 template <int PREC, int NK, int DIST = H_DIST, bool OWN = false>
 __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx,
-                                           HRing<DIST> *R = nullptr) {
+                                           HRing<DIST> *R = nullptr, const Drain *D = nullptr) {
     PT(g, 3);
     PT_COUNT(g, 5);
     if constexpr (PREC == 0) {
@@ -1017,7 +1057,8 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
                 acc[r][c] *= sa[c];
             }
         Fair *F = g.fair.prog ? &g.fair : nullptr;
-        if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
+        if (R && D) gemm_f16_primed<NK / 2, DIST, true>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F, D);
+        else if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
         else gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
@@ -1174,10 +1215,18 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
             lds_barrier();
     };
+    // PNR_SAVE_DRAIN: the fp32 save of a published image streams out of LDS during the next GEMM
+    // (Drain, gemm_f16_primed); the publish keeps only the sign masks
+    constexpr bool DRAIN_ON = PNR_SAVE_DRAIN && PREC == 3 && !PZ && !MARCH;
+    Drain dr;
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (a.save) {
-            save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
+            if constexpr (!DRAIN_ON) save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
             save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
+        }
+        if constexpr (DRAIN_ON) {
+            dr.base = a.save ? sv_slot(save_idx) + (row0 + tile * COLS) * H : nullptr;
+            dr.n_cols = !a.save ? 0 : P - tile * COLS < COLS ? (int)(P - tile * COLS) : COLS;
         }
 #ifdef PNR_GEMM_ONLY
         {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
@@ -1204,6 +1253,16 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         } else {
             store_relu(acc, inbuf, wave, lane);
         }
+    };
+
+    if constexpr (DRAIN_ON) {
+        dr.p0 = P0;
+        dr.ecol = ecol;
+        dr.wave = __builtin_amdgcn_readfirstlane(wave);
+    }
+    auto drain_arg = [&]() -> const Drain * {
+        if constexpr (DRAIN_ON) return &dr;
+        return nullptr;
     };
 
 #ifdef PNR_GEMM_ONLY
@@ -1503,7 +1562,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 PT(gc, 16);
                 set_bias(h, nb0, false);
                 layer_gemm<PREC, NKB, KD, PREC == 3>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
-                                          PREC == 3 ? &R0 : nullptr);
+                                          PREC == 3 ? &R0 : nullptr, drain_arg());
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
                 const float *w1p = PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats;
@@ -1515,7 +1574,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 PT(gc, 16);
                 set_bias(x, nb1, true);
                 layer_gemm<PREC, NKB, KD, PREC == 3>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
-                                          PREC == 3 ? &R1 : nullptr);
+                                          PREC == 3 ? &R1 : nullptr, drain_arg());
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -1560,7 +1619,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 16);
             set_bias(h, nb0, false);
             layer_gemm<PREC, NKB, KD, PREC == 3>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
-                                      PREC == 3 ? &R0 : nullptr);
+                                      PREC == 3 ? &R0 : nullptr, drain_arg());
             pre_publish_sync();
             HRing<KD> R1;
             const float *w1p = PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats;
@@ -1572,7 +1631,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 16);
             set_bias(x, nb1, true);
             layer_gemm<PREC, NKB, KD, PREC == 3>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
-                                      PREC == 3 ? &R1 : nullptr);
+                                      PREC == 3 ? &R1 : nullptr, drain_arg());
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier

@@ -5,8 +5,8 @@ The trunk's training-mode layers (encoder.py:135-149 over torchvision's BasicBlo
 output, running mean / variance (momentum, unbiased variance), num_batches_tracked, and the
 gradients of the map, the residual, gamma and beta.  Tolerance: fp32 rounding of the
 normalisation (torch reduces in fp32 Welford, the kernels in double): outputs within 2e-5 of
-their max-abs, gradients within 1e-4 of their max-abs (dy: of its terms' scale gamma invstd |dz|),
-running statistics within 1e-5.
+their max-abs or of gamma invstd |y| (the conditioning of y - mean in fp32), gradients within 1e-4
+of their max-abs (dy: of its terms' scale gamma invstd |dz|), running statistics within 1e-5.
 """
 import copy
 
@@ -51,7 +51,11 @@ def test_fused_batchnorm_matches_torch(shape, relu, add):
         o = o + ir
     outr = torch.relu(o) if relu else o
     assert out.is_contiguous(memory_format=torch.channels_last)
-    assert _rel(out, outr) < 2e-5
+    # fp32 conditioning of the normalisation: y - mean rounds at the scale of |y|, so the output
+    # error scales with gamma invstd |y| (large at M = 2 where the two values of a channel are close)
+    var = y0.double().var(dim=(0, 2, 3), unbiased=False)
+    gis = (bn.weight.double().abs() / (var + bn.eps).sqrt()).max().item()
+    assert (out - outr).abs().max().item() < 2e-5 * max(outr.abs().max().item(), gis * y0.abs().max().item())
     assert _rel(bn.running_mean, ref.running_mean) < 1e-5
     assert _rel(bn.running_var, ref.running_var) < 1e-5
     assert int(bn.num_batches_tracked) == int(ref.num_batches_tracked) == 8
@@ -61,8 +65,7 @@ def test_fused_batchnorm_matches_torch(shape, relu, add):
     outr.backward(dout)
     # dy is a difference of terms of size gamma invstd |dz|: measured against that scale (at M = 2
     # the exact dy is 0 and both sides are rounding noise of it)
-    var = y0.double().var(dim=(0, 2, 3), unbiased=False)
-    term = ((bn.weight.double().abs() / (var + bn.eps).sqrt()).max() * dout.abs().max()).item()
+    term = gis * dout.abs().max().item()
     assert (y.grad - yr.grad).abs().max().item() < 1e-4 * max(yr.grad.abs().max().item(), term)
     assert _rel(bn.weight.grad, ref.weight.grad) < 1e-4
     assert _rel(bn.bias.grad, ref.bias.grad) < 1e-4
