@@ -34,7 +34,8 @@ extern "C" {
                                5: pnr_latent_channels_last_nhwc;
                                6: pnr_fold_batchnorm;
                                7: pnr_batchnorm_train_forward / _backward,
-                                  pnr_latent_channels_last_backward */
+                                  pnr_latent_channels_last_backward,
+                                  pnr_points_input_backward_masked */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -414,6 +415,16 @@ int pnr_composite_backward(const float *z, const float *raw, const float *rays, 
 int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
                               const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
                               const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream);
+
+/* pnr_points_input_backward with z_mask (n_rays * k bytes, may be NULL = every point): d_z is
+ * computed only where z_mask is nonzero and written 0 elsewhere.  The fine pass's depths are the
+ * sort of [importance samples (no gradient), depth samples (gradient to the coarse depth)]
+ * (nerf.py:150-161, 292), so only the depth samples' dL/dz reaches the graph; the mask skips the
+ * latent-corner reads of the others (ABI 7). */
+int pnr_points_input_backward_masked(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                                     const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
+                                     const float *d_zlat, float *d_latent, float *d_z, const uint8_t *z_mask,
+                                     pnr_stream_t stream);
 
 /* Bytes of the transposed (backward) weight pack of an f16x3 model (precision
  * PNR_PREC_F16X3); 0 for an invalid desc or another precision. */

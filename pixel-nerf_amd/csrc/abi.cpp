@@ -48,7 +48,7 @@ int launch_composite_bwd(const float *, const float *, const float *, int64_t, i
                          const float *, const float *, float *, float *, hipStream_t);
 int launch_points_in_bwd(const float *, const float *, int, int64_t, int64_t, int, const float *, const float *,
                          int, int, float, float, const float *, int, const float *, const float *, float *,
-                         float *, hipStream_t);
+                         float *, const uint8_t *, hipStream_t);
 int launch_point_mlp(const pnr_scene &, const pnr_mlp_desc &, const void *, const float *,
                      const float *, int, int64_t, const float *, const float *, int64_t, int64_t,
                      float *, float *, hipStream_t, float *save = nullptr, const float *proj = nullptr,
@@ -230,9 +230,10 @@ int pnr_composite_backward(const float *z, const float *raw, const float *rays, 
                                 (hipStream_t)stream);
 }
 
-int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
-                              const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
-                              const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream) {
+int pnr_points_input_backward_masked(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                                     const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
+                                     const float *d_zlat, float *d_latent, float *d_z, const uint8_t *z_mask,
+                                     pnr_stream_t stream) {
     int rc = check_scene(scene);
     if (rc) return rc;
     if ((rc = check_desc_for_scene(desc, scene))) return rc;
@@ -242,7 +243,14 @@ int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, 
     return launch_points_in_bwd(rays->rays, z, k, rays->rays_per_obj, rays->n_rays * k, scene->n_views, scene->cams,
                                 scene->latent, scene->latent_h, scene->latent_w, scene->image_w,
                                 scene->image_h, static_cast<const float *>(packed), desc->pe_n, d_feat,
-                                d_zlat, d_latent, d_z, (hipStream_t)stream);
+                                d_zlat, d_latent, d_z, z_mask, (hipStream_t)stream);
+}
+
+int pnr_points_input_backward(const pnr_scene *scene, const pnr_mlp_desc *desc, const void *packed,
+                              const pnr_rays *rays, const float *z, int32_t k, const float *d_feat,
+                              const float *d_zlat, float *d_latent, float *d_z, pnr_stream_t stream) {
+    return pnr_points_input_backward_masked(scene, desc, packed, rays, z, k, d_feat, d_zlat, d_latent, d_z, nullptr,
+                                            stream);
 }
 
 size_t pnr_mlp_packed_t_bytes(const pnr_mlp_desc *desc) {

@@ -654,6 +654,9 @@ struct Fair {
 #ifndef PNR_SAVE_DRAIN
 #define PNR_SAVE_DRAIN 0
 #endif
+#ifndef PNR_DRAIN_AT
+#define PNR_DRAIN_AT 0   // where in the k-step (0 / 1: first, with / without a schedule barrier; 2 / 3: after the first / last ring load)
+#endif
 struct Drain {
     float *base;            // save slot row of the tile's column 0 (uniform)
     const _Float16 *p0;     // the image's P0 (P1 = p0 + PART_HALVES)
@@ -693,9 +696,9 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
         constexpr bool tail = decltype(tail_tag)::value;
         const int kr = ks & (NKS - 1);
         // the drain first: the previous k-step's B fragments are dead here (32 fewer live VGPRs)
-        if constexpr (DRAIN) {
+        if constexpr (DRAIN && PNR_DRAIN_AT <= 1) {
             drain_step(*D, kr);
-            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (PNR_DRAIN_AT == 0) __builtin_amdgcn_sched_barrier(0);
         }
         h8 b0[CT], b1[CT];
 #pragma unroll
@@ -708,6 +711,9 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
             const int tn = ph * RTW + r + DIST;            // prefetch target, relative to the iteration
             if (!tail || tn < U * RTW)
                 hring_load(R, wp, tn % H_RING, (ks - ph + tn / RTW) & (NKS - 1), tn % RTW);
+            if constexpr (DRAIN && PNR_DRAIN_AT >= 2) {
+                if (r == (PNR_DRAIN_AT == 2 ? 0 : RTW - 1)) drain_step(*D, kr);
+            }
             __builtin_amdgcn_sched_barrier(0);
             const h8 *a = R.ra[(ph * RTW + r) % H_RING];
 #pragma unroll

@@ -184,7 +184,8 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
     const float *__restrict__ rays, const float *__restrict__ zs, int K, int64_t rays_per_obj,
     int64_t n_points, int ns, const float *__restrict__ cams, const float *__restrict__ latent, int hl, int wl,
     float img_w, float img_h, const float *__restrict__ pe, int pe_n, const float *__restrict__ d_feat,
-    const float *__restrict__ d_zlat, float *__restrict__ d_latent, float *__restrict__ d_z) {
+    const float *__restrict__ d_zlat, float *__restrict__ d_latent, float *__restrict__ d_z,
+    const uint8_t *__restrict__ z_mask) {
     const int lane = threadIdx.x & 63;
     const int64_t p0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RUN;
     if (p0 >= n_points) return;
@@ -215,6 +216,8 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
         float dix_run = 0.f, diy_run = 0.f;   // lane j: point j's d ix / d iy (wave sums)
         for (int j = 0; j < n_run; ++j) {
             const int64_t p = p0 + j;
+            // the depth chain only where a caller needs dL / dz (z_mask: the fine pass's depth samples)
+            const bool need_z = d_z && (!z_mask || z_mask[p]);   // wave-uniform
             const PointGeo G = point_geo(rays, zs, K, rays_per_obj, cams, hl, wl, img_w, img_h, p, ns, v);
             const float we = sub_rn(G.ix, floorf(G.ix)), wn = sub_rn(G.iy, floorf(G.iy));
             const float wnw = mul_rn(sub_rn(1.f, wn), sub_rn(1.f, we)), wne = mul_rn(sub_rn(1.f, wn), we);
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
                 f4 gv;
 #pragma unroll
                 for (int q = 0; q < 4; ++q) gv[q] = gz[ch + q * 64];
-                if (d_z) {   // the latent corners only feed d ix / d iy (the depth chain)
+                if (need_z) {   // the latent corners only feed d ix / d iy (the depth chain)
                     f4 l00, l01, l10, l11;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -259,7 +262,7 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
                 acc[2][half] += wsw * gv;
                 acc[3][half] += wse * gv;
             }
-            if (d_z) {
+            if (need_z) {
                 dwe = wave_sum_dpp(dwe);
                 dwn = wave_sum_dpp(dwn);
                 if (lane == j) { dix_run = dwe; diy_run = dwn; }
@@ -269,6 +272,7 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
         if (!d_z || lane >= n_run) continue;
         // lane j: the dL/dz chain of point p0 + j through view v
         const int64_t p = p0 + lane;
+        if (z_mask && !z_mask[p]) continue;   // d_z written 0 below
         const PointGeo G = point_geo(rays, zs, K, rays_per_obj, cams, hl, wl, img_w, img_h, p, ns, v);
         const float *ray = rays + (p / K) * 8;
         const float *cam = cams + (((p / K) / rays_per_obj) * ns + v) * 16;
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(256) void k_points_in_bwd(
         }
         dz_sum = v == 0 ? dzs : dz_sum + dzs;
     }
-    if (d_z && lane < n_run) d_z[p0 + lane] = dz_sum;
+    if (d_z && lane < n_run) d_z[p0 + lane] = (z_mask && !z_mask[p0 + lane]) ? 0.f : dz_sum;
 }
 
 // ---------------------------------------------------------------------------
@@ -325,12 +329,12 @@ int launch_composite_bwd(const float *z, const float *raw, const float *rays, in
 int launch_points_in_bwd(const float *rays, const float *zs, int K, int64_t rays_per_obj, int64_t n_points,
                          int ns, const float *cams, const float *latent, int hl, int wl, float img_w, float img_h,
                          const float *pe, int pe_n, const float *d_feat, const float *d_zlat,
-                         float *d_latent, float *d_z, hipStream_t st) {
+                         float *d_latent, float *d_z, const uint8_t *z_mask, hipStream_t st) {
     if (n_points == 0) return PNR_OK;
     const int64_t waves = (n_points + RUN - 1) / RUN;
     hipLaunchKernelGGL(k_points_in_bwd, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, rays, zs, K,
                        rays_per_obj, n_points, ns, cams, latent, hl, wl, img_w, img_h, pe, pe_n, d_feat, d_zlat,
-                       d_latent, d_z);
+                       d_latent, d_z, z_mask);
     return launch_ok("points_in_bwd") ? PNR_OK : PNR_ERR_HIP;
 }
 

@@ -121,6 +121,9 @@ SIGNATURES = {
     "pnr_points_input_backward": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp,
                                           ctypes.POINTER(Rays), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
                                           c_vp]),
+    "pnr_points_input_backward_masked": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp,
+                                                 ctypes.POINTER(Rays), c_vp, c_i32, c_vp, c_vp, c_vp, c_vp,
+                                                 c_vp, c_vp]),
     "pnr_mlp_packed_t_bytes": (c_size, [ctypes.POINTER(MlpDesc)]),
     "pnr_mlp_pack_t": (c_i32, [ctypes.POINTER(MlpWeights), c_vp, c_vp, c_size, c_vp]),
     "pnr_mlp_backward": (c_i32, [ctypes.POINTER(MlpDesc), c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,

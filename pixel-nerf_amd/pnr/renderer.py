@@ -196,7 +196,7 @@ class NeRFRenderer(torch.nn.Module):
         With noise_std > 0 in training mode, sigma noise is added before compositing
         (nerf.py:225-226) and the draws follow the reference's order: u_coarse, coarse
         noise, u_fine, u_fine_jit, n_depth, fine noise."""
-        from .train import Composite, RenderPoints, mlp_params
+        from .train import Composite, FinePass, RenderPoints, mlp_params
 
         r = net.hip_unsupported_reason()
         if r:
@@ -241,9 +241,12 @@ class NeRFRenderer(torch.nn.Module):
             if kfd > 0:
                 z_d = d_c.unsqueeze(1).repeat((1, kfd)) + n_d * self.depth_std
                 parts.append(torch.max(torch.min(z_d, rays[:, -1:]), rays[:, -2:-1]))
-            z_f = torch.sort(torch.cat(parts, -1), -1)[0].contiguous()
+            z_f, order = torch.sort(torch.cat(parts, -1), -1)
+            z_f = z_f.contiguous()
+            # only the depth samples' dL/dz reaches the graph (the importance samples carry none)
+            fine = FinePass(order >= z_ci.shape[1] if kfd > 0 else None)
             p_f = mlp_params(net.mlp_fine) if net.mlp_fine is not None else p_c
-            raw_f = add_noise(RenderPoints.apply(net, False, rays, z_f, lat, *p_f))
+            raw_f = add_noise(RenderPoints.apply(net, fine, rays, z_f, lat, *p_f))
             w_f, rgb_f, d_f = Composite.apply(z_f, raw_f.contiguous(), rays, self.white_bkgd)
             outputs.fine = self._pack_out(w_f, rgb_f, d_f, sb, want_weights, z_f)
         return outputs

@@ -287,6 +287,19 @@ def mlp_backward_fused(mlp, code, precision, save, d_o, P, ns=1, wgrad_arith="f1
     return g, d_feat, dzl
 
 
+class FinePass:
+    """The ``coarse`` argument of RenderPoints for a fine pass (false) carrying ``z_mask`` (n_rays,
+    k) bool: the points whose dL/dz reaches the graph -- the depth samples of the sorted
+    [importance, depth] fine depths (nerf.py:150-161, 292); the input backward computes the depth
+    chain only there (``pnr_points_input_backward_masked``)."""
+
+    def __init__(self, z_mask=None):
+        self.z_mask = z_mask
+
+    def __bool__(self):
+        return False
+
+
 class RenderPoints(torch.autograd.Function):
     """raw (B, K, 4) = PixelNeRFNet at o + z d (models.py:146-266, via nerf.py:182-216),
     differentiable in z, the encoder latent (channels-last) and the MLP parameters."""
@@ -321,6 +334,7 @@ class RenderPoints(torch.autograd.Function):
         _ev_end("forward", e0, forward_flop(mlp, P, ns))
         ctx.save_for_backward(rays, z, out, save, latent_cl)
         ctx.net, ctx.mlp, ctx.desc, ctx.packed, ctx.params = net, mlp, desc, packed, params
+        ctx.z_mask = getattr(coarse, "z_mask", None)
         return out.view(B, K, 4)
 
     @staticmethod
@@ -349,11 +363,13 @@ class RenderPoints(torch.autograd.Function):
             _on_device(z.device, "packed rays d_feat d_zlat d_latent cams latent", ctx.packed, rays, d_feat,
                        d_zlat, d_lat, net.cams, net.encoder.latent_cl)
             r = _lib.Rays(_lib.ptr(rays), B, B // net.num_objs)
-            _lib.check(lib.pnr_points_input_backward(net.hip_scene(), ctx.desc, _lib.ptr(ctx.packed), r,
-                                                     _lib.ptr(z), K, _lib.ptr(d_feat.contiguous()),
-                                                     _lib.ptr(d_zlat.contiguous()), _lib.ptr(d_lat),
-                                                     _lib.ptr(d_z), _lib.stream_of(z.device)),
-                       "pnr_points_input_backward")
+            zm = getattr(ctx, "z_mask", None)
+            if zm is not None:
+                zm = zm.reshape(P).to(device=z.device, dtype=torch.uint8).contiguous()
+            _lib.check(lib.pnr_points_input_backward_masked(
+                net.hip_scene(), ctx.desc, _lib.ptr(ctx.packed), r, _lib.ptr(z), K, _lib.ptr(d_feat.contiguous()),
+                _lib.ptr(d_zlat.contiguous()), _lib.ptr(d_lat), _lib.ptr(d_z), _lib.ptr(zm) if need_z else None,
+                _lib.stream_of(z.device)), "pnr_points_input_backward_masked")
         grads = [g.get(p) for p in ctx.params]
         return (None, None, None, d_z.view(B, K) if need_z else None, d_lat, *grads)
 

@@ -111,6 +111,27 @@ def test_training_step_gradients_match_oracle(precision, tol, wgrad_arith):
     compare(case(), precision, tol, wgrad_arith)
 
 
+def test_fine_pass_depth_mask_changes_no_gradient(monkeypatch):
+    """The fine pass's input backward computes dL/dz only for the depth samples (FinePass z_mask,
+    pnr_points_input_backward_masked): every gradient equals the unmasked backward's (the other
+    points' dL/dz never reaches the graph), up to the latent scatter's atomic order."""
+    from pnr import train
+
+    cs = case()
+    loss_m, got = hip_grads(cs, "f16x3")
+    orig = train.FinePass.__init__
+
+    def unmasked(self, z_mask=None):
+        orig(self, None)
+
+    monkeypatch.setattr(train.FinePass, "__init__", unmasked)
+    loss_u, ref = hip_grads(cs, "f16x3")
+    assert loss_m == loss_u
+    for k in ref:
+        a, b = got[k].double(), ref[k].double()
+        assert float((a - b).abs().max()) <= 1e-6 * float(b.abs().max()) + 1e-12, k
+
+
 def conditioned(sd, margin=3.0, scale=0.1):
     """The state dict with every ReLU input held away from zero: weights scaled by `scale`,
     lin_in / fc_0 biases +-margin by a fixed sign pattern, the other biases 0 (sigma's
