@@ -351,11 +351,40 @@ __device__ __forceinline__ int opaque_lane(int lane) {
     return lane;
 }
 
+// Activation-save stores (training forward).  PNR_SAVE_WT: write-through (sc1) buffer
+// stores, whose lines leave the XCD's L2 -- plain and nt stores keep them (MI355X_MICROARCH.md,
+// store flavours), so each publish's 128 KB per workgroup of save data evicted the weight stream
+// the GEMMs read from that L2.  Base and size are wave-uniform (the tile's first row of the slot and
+// its valid rows); the buffer range check drops the stores of columns past n_points.
+#ifndef PNR_SAVE_WT
+#define PNR_SAVE_WT 0
+#endif
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void save_store16(float *base, int64_t n_bytes, int off_bytes, const f4 &v) {
+    auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)n_bytes, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, off_bytes, 0, 16);
+}
+// valid bytes of a tile's rows in a save region of `width` floats per row
+__device__ __forceinline__ int64_t tile_bytes(int64_t tile, int64_t n_points, int width) {
+    const int64_t n = n_points - tile * COLS;
+    return (n <= 0 ? 0 : n >= COLS ? COLS : n) * width * 4;
+}
+
 // relu(acc) of this wave's rows -> save slot [point][512] (points of this tile < n_points)
+template <bool WT>
 __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
+    if constexpr (WT) {
+    float *base = slot + tile * COLS * H;
+    const int64_t nb = tile_bytes(tile, n_points, H);
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+        for (int r = 0; r < RTW; ++r)
+            save_store16(base, nb, 4 * ((16 * c + cl) * H + 16 * (RTW * wave + r) + 4 * g), relu4(acc[r][c]));
+    } else {
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
@@ -365,6 +394,7 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
             const f4 v = acc[r][c];
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = relu4(v);
         }
+    }
     }
 }
 
@@ -644,47 +674,9 @@ struct Fair {
     int *prog;   // LDS: iteration count per wave (8 ints)
     int wave, it, mate;
 };
-// Activation save drained from the LDS image during the GEMM that reads it (training forward,
-// PNR_SAVE_DRAIN): lane l of wave w owns column 8 w + (l >> 3) of the tile and, at k-step ks,
-// its 4 channels 32 ks + 4 (l & 7); the GEMM's k-step reads them from P0 / P1 beside its own B
-// fragments and stores (P0 + P1) 2^-e_col (the value the GEMM multiplies) as one 16-B store issued
-// after the k-step's last ring load, so the save streams out one store per lane per k-step
-// instead of the publish's 16-store burst whose completion the next ring waits queued behind
-// (vmcnt counts stores and loads in order).
-#ifndef PNR_SAVE_DRAIN
-#define PNR_SAVE_DRAIN 0
-#endif
-#ifndef PNR_DRAIN_AT
-#define PNR_DRAIN_AT 0   // where in the k-step (0 / 1: first, with / without a schedule barrier; 2 / 3: after the first / last ring load)
-#endif
-struct Drain {
-    float *base;            // save slot row of the tile's column 0 (uniform)
-    const _Float16 *p0;     // the image's P0 (P1 = p0 + PART_HALVES)
-    const int *ecol;        // the image's column exponents
-    int wave;               // (uniform)
-    int n_cols;             // columns of the tile that are points (uniform)
-};
-// this lane's part of k-step ks: everything recomputed from the lane id (no registers held
-// across the GEMM's k-steps, where the accumulators and the ring fill the register file)
-__device__ __forceinline__ void drain_step(const Drain &D, int ks) {
-    const int ln = (int)__lane_id(), j = ln & 7, col = 8 * D.wave + (ln >> 3);
-    if (col >= D.n_cols) return;
-    const _Float16 *src = D.p0 + col * ROWH + 32 * ks + 8 * ((j >> 1) ^ ((col >> 2) & 3)) + 4 * (j & 1);
-    const u2 q0 = *reinterpret_cast<const u2 *>(src);
-    const u2 q1 = *reinterpret_cast<const u2 *>(src + PART_HALVES);
-    const float inv = __builtin_ldexpf(1.f, -D.ecol[col]);
-    const f2 a0 = __builtin_convertvector(__builtin_bit_cast(h2, q0.x), f2);
-    const f2 a1 = __builtin_convertvector(__builtin_bit_cast(h2, q0.y), f2);
-    const f2 c0 = __builtin_convertvector(__builtin_bit_cast(h2, q1.x), f2);
-    const f2 c1 = __builtin_convertvector(__builtin_bit_cast(h2, q1.y), f2);
-    *reinterpret_cast<f4 *>(D.base + col * H + 32 * ks + 4 * j) =
-        f4{a0.x + c0.x, a0.y + c0.y, a1.x + c1.x, a1.y + c1.y} * inv;
-}
-
-template <int NKS, int DIST = H_DIST, bool DRAIN = false>
+template <int NKS, int DIST = H_DIST>
 __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const float *__restrict__ wp,
-                                                const _Float16 *pb0, const _Float16 *pb1, Fair *F = nullptr,
-                                                const Drain *D = nullptr) {
+                                                const _Float16 *pb0, const _Float16 *pb1, Fair *F = nullptr) {
     constexpr int H_RING = HRing<DIST>::slots;   // register ring slots
     static_assert(DIST < H_RING && H_RING % RTW == 0, "ring");
     constexpr int U = H_RING / RTW;   // k-steps per loop iteration (static ring slots)
@@ -694,13 +686,8 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
     auto kstep = [&](int ks, auto ph_tag, auto tail_tag) {
         constexpr int ph = decltype(ph_tag)::value;
         constexpr bool tail = decltype(tail_tag)::value;
-        const int kr = ks & (NKS - 1);
-        // the drain first: the previous k-step's B fragments are dead here (32 fewer live VGPRs)
-        if constexpr (DRAIN && PNR_DRAIN_AT <= 1) {
-            drain_step(*D, kr);
-            if constexpr (PNR_DRAIN_AT == 0) __builtin_amdgcn_sched_barrier(0);
-        }
         h8 b0[CT], b1[CT];
+        const int kr = ks & (NKS - 1);
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             b0[c] = *reinterpret_cast<const h8 *>(pb0 + c * 16 * ROWH + 32 * kr);
@@ -711,9 +698,6 @@ __device__ __forceinline__ void gemm_f16_primed(Acc &acc, HRing<DIST> &R, const 
             const int tn = ph * RTW + r + DIST;            // prefetch target, relative to the iteration
             if (!tail || tn < U * RTW)
                 hring_load(R, wp, tn % H_RING, (ks - ph + tn / RTW) & (NKS - 1), tn % RTW);
-            if constexpr (DRAIN && PNR_DRAIN_AT >= 2) {
-                if (r == (PNR_DRAIN_AT == 2 ? 0 : RTW - 1)) drain_step(*D, kr);
-            }
             __builtin_amdgcn_sched_barrier(0);
             const h8 *a = R.ra[(ph * RTW + r) % H_RING];
 #pragma unroll
@@ -1039,7 +1023,7 @@ __device__ __forceinline__ void add_stage(Acc &x, const float *stage, int wave, 
 // that publish's registers (g.ecl) instead of LDS, so the accumulator scaling does not wait on a read.
 template <int PREC, int NK, int DIST = H_DIST, bool OWN = false>
 __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, GemmCtx &g, int hidx,
-                                           HRing<DIST> *R = nullptr, const Drain *D = nullptr) {
+                                           HRing<DIST> *R = nullptr) {
     PT(g, 3);
     PT_COUNT(g, 5);
     if constexpr (PREC == 0) {
@@ -1063,8 +1047,7 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
                 acc[r][c] *= sa[c];
             }
         Fair *F = g.fair.prog ? &g.fair : nullptr;
-        if (R && D) gemm_f16_primed<NK / 2, DIST, true>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F, D);
-        else if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
+        if (R) gemm_f16_primed<NK / 2, DIST>(acc, *R, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
         else gemm_f16<NK / 2, DIST>(acc, layer_base + opaque_lane((int)g.ws_off), g.pb0, g.pb1, F);
 #pragma unroll
         for (int r = 0; r < RTW; ++r)
@@ -1150,6 +1133,9 @@ __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const f
 // keeps its own register allocation
 template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
+    // write-through save stores in the training-forward kernel only (the ABI refuses a save with the
+    // projected latent or the march; their register plans stay those of the plain-store code)
+    constexpr bool SAVE_WT = PNR_SAVE_WT && !PZ && !MARCH;
     constexpr int KD = H_DIST;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
@@ -1221,18 +1207,10 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
 #endif
             lds_barrier();
     };
-    // PNR_SAVE_DRAIN: the fp32 save of a published image streams out of LDS during the next GEMM
-    // (Drain, gemm_f16_primed); the publish keeps only the sign masks
-    constexpr bool DRAIN_ON = PNR_SAVE_DRAIN && PREC == 3 && !PZ && !MARCH;
-    Drain dr;
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (a.save) {
-            if constexpr (!DRAIN_ON) save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
+            save_relu<SAVE_WT>(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
             save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
-        }
-        if constexpr (DRAIN_ON) {
-            dr.base = a.save ? sv_slot(save_idx) + (row0 + tile * COLS) * H : nullptr;
-            dr.n_cols = !a.save ? 0 : P - tile * COLS < COLS ? (int)(P - tile * COLS) : COLS;
         }
 #ifdef PNR_GEMM_ONLY
         {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
@@ -1259,16 +1237,6 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         } else {
             store_relu(acc, inbuf, wave, lane);
         }
-    };
-
-    if constexpr (DRAIN_ON) {
-        dr.p0 = P0;
-        dr.ecol = ecol;
-        dr.wave = __builtin_amdgcn_readfirstlane(wave);
-    }
-    auto drain_arg = [&]() -> const Drain * {
-        if constexpr (DRAIN_ON) return &dr;
-        return nullptr;
     };
 
 #ifdef PNR_GEMM_ONLY
@@ -1422,7 +1390,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     }
                     fv[i] = val;
                 }
-                if (a.save && p_raw < a.n_points) {
+                if (SAVE_WT && a.save) {
+#pragma unroll
+                    for (int i = 0; i < FPT / 4; ++i)
+                        save_store16(sv_f + (v * P + tile * COLS) * 64, tile_bytes(tile, P, 64),
+                                     4 * ((int)(p_raw - tile * COLS) * 64 + FPT * qt + 4 * i),
+                                     f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]});
+                }
+                if (!SAVE_WT && a.save && p_raw < a.n_points) {
 #pragma unroll
                     for (int i = 0; i < FPT / 4; ++i)
                         *reinterpret_cast<f4 *>(sv_f + (v * P + p_raw) * 64 + FPT * qt + 4 * i) =
@@ -1534,7 +1509,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                                   mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
                         if constexpr (PREC == 3) zh[half] = zz;
                         else *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
-                        if (a.save && blk == 0 && tile * COLS + cj < P)
+                        if (SAVE_WT && a.save && blk == 0)
+                            save_store16(sv_z + (v * P + tile * COLS) * H, tile_bytes(tile, P, H), 4 * (cj * H + ch), zz);
+                        if (!SAVE_WT && a.save && blk == 0 && tile * COLS + cj < P)
                             *reinterpret_cast<f4 *>(sv_z + (v * P + tile * COLS + cj) * H + ch) = zz;
                     }
                     if constexpr (PREC == 3) {
@@ -1568,7 +1545,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 PT(gc, 16);
                 set_bias(h, nb0, false);
                 layer_gemm<PREC, NKB, KD, PREC == 3>(h, PK() + L.off_l512 + (int64_t)(lz + 1) * L.layer_floats, gc, 2 + lz,
-                                          PREC == 3 ? &R0 : nullptr, drain_arg());
+                                          PREC == 3 ? &R0 : nullptr);
                 pre_publish_sync();
                 HRing<KD> R1;   // fc_1's
                 const float *w1p = PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats;
@@ -1580,7 +1557,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 PT(gc, 16);
                 set_bias(x, nb1, true);
                 layer_gemm<PREC, NKB, KD, PREC == 3>(x, PK() + L.off_l512 + (int64_t)(lz + 2) * L.layer_floats, gc, 3 + lz,
-                                          PREC == 3 ? &R1 : nullptr, drain_arg());
+                                          PREC == 3 ? &R1 : nullptr);
             }
             // ---- multi-view mean (combine_interleaved: sum over views, then / NS) --
             if (a.ns > 1) {
@@ -1625,7 +1602,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 16);
             set_bias(h, nb0, false);
             layer_gemm<PREC, NKB, KD, PREC == 3>(h, PK() + L.off_l512 + (int64_t)l0 * L.layer_floats, gc, 1 + l0,
-                                      PREC == 3 ? &R0 : nullptr, drain_arg());
+                                      PREC == 3 ? &R0 : nullptr);
             pre_publish_sync();
             HRing<KD> R1;
             const float *w1p = PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats;
@@ -1637,7 +1614,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             PT(gc, 16);
             set_bias(x, nb1, true);
             layer_gemm<PREC, NKB, KD, PREC == 3>(x, PK() + L.off_l512 + (int64_t)(l0 + 1) * L.layer_floats, gc, 2 + l0,
-                                      PREC == 3 ? &R1 : nullptr, drain_arg());
+                                      PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
         if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier
@@ -1646,7 +1623,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             // no publish: the head reads relu(x) from the accumulators (below); only the
             // activation save of lin_out's input remains
             if (a.save) {
-                save_relu(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
+                save_relu<SAVE_WT>(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
                 save_mask(x, sv_mask + PS * 16 * (2 * L.n_blocks), tile, P, wave, lane);
             }
         } else {
