@@ -9,7 +9,8 @@
 // Here one BatchNorm(+add)(+relu) is two launches each way, on channels-last (NHWC) fp32 maps viewed
 // as (M = N H W) x C:
 //   k_bn_stats      per row block: sum y and sum y^2 per channel (double) into its partial slot; the
-//                   last block to finish (a device-scope arrival counter) reduces the partials in
+//                   last block to finish (a device-scope arrival counter, write-through partials,
+//                   no fences) reduces the partials in
 //                   block order -- mean, biased variance, invstd = 1 / sqrt(var + eps), the running
 //                   statistics (momentum, unbiased variance) and num_batches_tracked, as torch --
 //                   and re-arms the counter;
@@ -31,9 +32,27 @@ constexpr int ROWS = 128;   // rows of one partial block
 
 constexpr size_t COUNTER_BYTES = 256;
 
+// The cross-block hand-off of the column sums without fences (MI355X_MICROARCH.md, the valid
+// forms of an in-launch hand-off): every partial is stored write-through (an agent-scope relaxed
+// 8-B store: global_store sc1), every storing wave drains its stores (vmcnt 0) before the block's
+// barrier, ONE lane then adds to the arrival counter (agent scope), the block whose add returns
+// nb - 1 is last, and it reads the partials with agent-scope relaxed loads (global_load sc1).  An
+// agent-scope __threadfence costs ~3.5 us per block; two of them made these launches slower than
+// MIOpen's (profiles/r5j).
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ void st_wt(double *p, double v) {
+    __hip_atomic_store((gu64 *)(p), (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double *p) {
+    return __longlong_as_double((long long)__hip_atomic_load((gu64 *)(const_cast<double *>(p)),
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 // Column sums of a (M x C) block of rows: thread t owns channel group g = t % G (4 channels) and
 // row slot r = t / G of R = NTHR / G; the slots combine in slot order (deterministic).  Writes the
-// block's [sum a | sum b] (2 C doubles) to its partial slot.
+// block's [sum a | sum b] (2 C doubles) to its partial slot, write-through.
 __device__ __forceinline__ void store_block_partial(const double (&s)[4], const double (&q)[4], int C,
                                                     double *red, double *p) {
     const int G = C >> 2, R = NTHR / G, t = threadIdx.x;
@@ -49,26 +68,25 @@ __device__ __forceinline__ void store_block_partial(const double (&s)[4], const 
             for (int e = 0; e < 8; ++e) red[t * 8 + e] += red[(rr * G + t) * 8 + e];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            p[4 * t + e] = red[t * 8 + e];
-            p[C + 4 * t + e] = red[t * 8 + 4 + e];
+            st_wt(p + 4 * t + e, red[t * 8 + e]);
+            st_wt(p + C + 4 * t + e, red[t * 8 + 4 + e]);
         }
     }
 }
 
-// Arrival: true in the block that finishes last (it then sees every block's partial slot).
+// Arrival: true in the block that finishes last (it then reads every block's partial slot with ld_wt).
 __device__ __forceinline__ bool last_block(unsigned *counter, int nb) {
     __shared__ int is_last;
-    __threadfence();   // this block's partial slot, visible device-wide before the arrival
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's write-through partial stores done
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prev = __hip_atomic_fetch_add((gu32 *)(counter), 1u, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
         is_last = prev == (unsigned)(nb - 1);
+        if (is_last) __hip_atomic_store((gu32 *)(counter), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (!is_last) return false;
-    __threadfence();
-    if (threadIdx.x == 0) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
+    return is_last != 0;
 }
 
 // Channel totals over the nb partial slots, in slot order within J = NTHR / C interleaved slices
@@ -80,8 +98,8 @@ __device__ __forceinline__ void reduce_partials(const double *part, int nb, int 
         const int J = NTHR / C, c = t % C, j = t / C;
         double s = 0.0, q = 0.0;
         for (int b = j; b < nb; b += J) {
-            s += part[(int64_t)b * 2 * C + c];
-            q += part[(int64_t)b * 2 * C + C + c];
+            s += ld_wt(part + (int64_t)b * 2 * C + c);
+            q += ld_wt(part + (int64_t)b * 2 * C + C + c);
         }
         __syncthreads();   // red reused
         red[2 * t] = s;
@@ -98,8 +116,8 @@ __device__ __forceinline__ void reduce_partials(const double *part, int nb, int 
         for (int c = t; c < C; c += NTHR) {
             double s = 0.0, q = 0.0;
             for (int b = 0; b < nb; ++b) {
-                s += part[(int64_t)b * 2 * C + c];
-                q += part[(int64_t)b * 2 * C + C + c];
+                s += ld_wt(part + (int64_t)b * 2 * C + c);
+                q += ld_wt(part + (int64_t)b * 2 * C + C + c);
             }
             fin(c, s, q);
         }

@@ -351,40 +351,11 @@ __device__ __forceinline__ int opaque_lane(int lane) {
     return lane;
 }
 
-// Activation-save stores (training forward).  PNR_SAVE_WT: write-through (sc1) buffer
-// stores, whose lines leave the XCD's L2 -- plain and nt stores keep them (MI355X_MICROARCH.md,
-// store flavours), so each publish's 128 KB per workgroup of save data evicted the weight stream
-// the GEMMs read from that L2.  Base and size are wave-uniform (the tile's first row of the slot and
-// its valid rows); the buffer range check drops the stores of columns past n_points.
-#ifndef PNR_SAVE_WT
-#define PNR_SAVE_WT 0
-#endif
-typedef unsigned u4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void save_store16(float *base, int64_t n_bytes, int off_bytes, const f4 &v) {
-    auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)n_bytes, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, v), rs, off_bytes, 0, 16);
-}
-// valid bytes of a tile's rows in a save region of `width` floats per row
-__device__ __forceinline__ int64_t tile_bytes(int64_t tile, int64_t n_points, int width) {
-    const int64_t n = n_points - tile * COLS;
-    return (n <= 0 ? 0 : n >= COLS ? COLS : n) * width * 4;
-}
-
 // relu(acc) of this wave's rows -> save slot [point][512] (points of this tile < n_points)
-template <bool WT>
 __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t tile, int64_t n_points,
                                           int wave, int lane) {
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
-    if constexpr (WT) {
-    float *base = slot + tile * COLS * H;
-    const int64_t nb = tile_bytes(tile, n_points, H);
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-        for (int r = 0; r < RTW; ++r)
-            save_store16(base, nb, 4 * ((16 * c + cl) * H + 16 * (RTW * wave + r) + 4 * g), relu4(acc[r][c]));
-    } else {
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
@@ -394,7 +365,6 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
             const f4 v = acc[r][c];
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = relu4(v);
         }
-    }
     }
 }
 
@@ -1133,9 +1103,6 @@ __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const f
 // keeps its own register allocation
 template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
-    // write-through save stores in the training-forward kernel only (the ABI refuses a save with the
-    // projected latent or the march; their register plans stay those of the plain-store code)
-    constexpr bool SAVE_WT = PNR_SAVE_WT && !PZ && !MARCH;
     constexpr int KD = H_DIST;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
@@ -1209,7 +1176,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     };
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (a.save) {
-            save_relu<SAVE_WT>(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
+            save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
             save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
         }
 #ifdef PNR_GEMM_ONLY
@@ -1390,14 +1357,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     }
                     fv[i] = val;
                 }
-                if (SAVE_WT && a.save) {
-#pragma unroll
-                    for (int i = 0; i < FPT / 4; ++i)
-                        save_store16(sv_f + (v * P + tile * COLS) * 64, tile_bytes(tile, P, 64),
-                                     4 * ((int)(p_raw - tile * COLS) * 64 + FPT * qt + 4 * i),
-                                     f4{fv[4 * i], fv[4 * i + 1], fv[4 * i + 2], fv[4 * i + 3]});
-                }
-                if (!SAVE_WT && a.save && p_raw < a.n_points) {
+                if (a.save && p_raw < a.n_points) {
 #pragma unroll
                     for (int i = 0; i < FPT / 4; ++i)
                         *reinterpret_cast<f4 *>(sv_f + (v * P + p_raw) * 64 + FPT * qt + 4 * i) =
@@ -1509,9 +1469,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                                   mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
                         if constexpr (PREC == 3) zh[half] = zz;
                         else *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
-                        if (SAVE_WT && a.save && blk == 0)
-                            save_store16(sv_z + (v * P + tile * COLS) * H, tile_bytes(tile, P, H), 4 * (cj * H + ch), zz);
-                        if (!SAVE_WT && a.save && blk == 0 && tile * COLS + cj < P)
+                        if (a.save && blk == 0 && tile * COLS + cj < P)
                             *reinterpret_cast<f4 *>(sv_z + (v * P + tile * COLS + cj) * H + ch) = zz;
                     }
                     if constexpr (PREC == 3) {
@@ -1623,7 +1581,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             // no publish: the head reads relu(x) from the accumulators (below); only the
             // activation save of lin_out's input remains
             if (a.save) {
-                save_relu<SAVE_WT>(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
+                save_relu(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
                 save_mask(x, sv_mask + PS * 16 * (2 * L.n_blocks), tile, P, wave, lane);
             }
         } else {
