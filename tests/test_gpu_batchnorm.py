@@ -66,7 +66,11 @@ def test_fused_batchnorm_matches_torch(shape, relu, add):
     # dy is a difference of terms of size gamma invstd |dz|: measured against that scale (at M = 2
     # the exact dy is 0 and both sides are rounding noise of it)
     term = gis * dout.abs().max().item()
-    assert (y.grad - yr.grad).abs().max().item() < 1e-4 * max(yr.grad.abs().max().item(), term)
+    # ... plus x_hat's own rounding, amplified by invstd |y| (y - mean at the scale of |y|): large
+    # only when a channel's values nearly coincide (M = 2)
+    cond = (y0.abs().max().double() / (var + bn.eps).sqrt().min()).item()
+    tol = 1e-4 + 64 * 2.0 ** -24 * cond
+    assert (y.grad - yr.grad).abs().max().item() < tol * max(yr.grad.abs().max().item(), term)
     assert _rel(bn.weight.grad, ref.weight.grad) < 1e-4
     assert _rel(bn.bias.grad, ref.bias.grad) < 1e-4
     if add:
