@@ -33,8 +33,7 @@ extern "C" {
 #define PNR_ABI_VERSION 7   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
                                5: pnr_latent_channels_last_nhwc;
                                6: pnr_fold_batchnorm;
-                               7: pnr_batchnorm_train_forward / _backward,
-                                  pnr_latent_channels_last_backward,
+                               7: pnr_latent_channels_last_backward,
                                   pnr_points_input_backward_masked */
 
 typedef enum pnr_status {
@@ -351,33 +350,6 @@ typedef struct pnr_bn_fold {
  * reading the same array); max_elems = max n_out * per_out.  Replaces the per-encode BatchNorm
  * arithmetic of SpatialEncoder.forward in eval mode (encoder.py:135-149); ABI 6. */
 int pnr_fold_batchnorm(const pnr_bn_fold *folds, int32_t n_folds, int64_t max_elems, pnr_stream_t stream);
-
-/* Train-mode BatchNorm of one trunk layer on batch statistics, with its residual add and ReLU
- * (encoder.py:135-149 with the torchvision BasicBlock's relu(bn1(conv1 x)) / relu(bn2(conv2 h) +
- * idt) / downsample bn): y and out are channels-last (NHWC) fp32 maps viewed as M = N H W rows
- * of C channels (C a multiple of 4 with C / 4 dividing 256).
- *   forward:  mean / biased variance per channel over the M rows, invstd = 1 / sqrt(var + eps);
- *             out = [relu]((y - mean) invstd gamma + beta [+ idt]) (idt NULL: no add);
- *             running_mean / running_var (unbiased) updated with momentum and *num_batches_tracked
- *             advanced, as torch's BatchNorm2d in training mode (each NULL: skipped);
- *             stats (2 C floats) receives [mean | invstd] for the backward.
- *   backward: dz = dout [out > 0] (relu) or dout; d_beta = sum dz, d_gamma = sum dz x_hat;
- *             dy = gamma invstd (dz - d_beta / M - x_hat d_gamma / M); d_idt = dz (NULL: skipped).
- * Two launches each way; the block that finishes the column sums last reduces them (device-scope
- * arrival counters at the head of the workspace).  Reductions in double, in a fixed order
- * (deterministic).  Workspace: pnr_batchnorm_workspace_bytes(M, C), 256-byte aligned, its first
- * 256 bytes zero before the first call (every call leaves them zero: one workspace serves a
- * stream's successive calls).  Replaces torch BatchNorm2d (MIOpen) + relu + add in the
- * training encode (pnr.encoder); ABI 7. */
-size_t pnr_batchnorm_workspace_bytes(int64_t M, int32_t C);
-int pnr_batchnorm_train_forward(const float *y, const float *idt, const float *gamma, const float *beta,
-                                float *running_mean, float *running_var, int64_t *num_batches_tracked,
-                                int64_t M, int32_t C, float momentum, float eps, int32_t relu, float *out,
-                                float *stats, void *workspace, size_t workspace_bytes, pnr_stream_t stream);
-int pnr_batchnorm_train_backward(const float *y, const float *out, const float *dout, const float *gamma,
-                                 const float *stats, int64_t M, int32_t C, int32_t relu, float *dy, float *d_idt,
-                                 float *d_gamma, float *d_beta, void *workspace, size_t workspace_bytes,
-                                 pnr_stream_t stream);
 
 /* ---- training (autograd over the ray march) ------------ */
 /* Floats of the activation save of pnr_render_points for n_points rows; call it with

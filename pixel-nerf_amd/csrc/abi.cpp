@@ -37,11 +37,6 @@ int launch_wgrad(const float *const *, const float *const *, float *const *, int
 int launch_fold_bn(const pnr_bn_fold *, int, int64_t, hipStream_t);
 int launch_latent_cl_bwd(const float *, float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, int,
                          int, hipStream_t);
-size_t bn_workspace_bytes(int64_t, int);
-int launch_bn_forward(const float *, const float *, const float *, const float *, float *, float *, int64_t *, int64_t,
-                      int, float, float, int, float *, float *, void *, size_t, hipStream_t);
-int launch_bn_backward(const float *, const float *, const float *, const float *, const float *, int64_t, int, int,
-                       float *, float *, float *, float *, void *, size_t, hipStream_t);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
                      int, int, bool, hipStream_t);
 int launch_composite_bwd(const float *, const float *, const float *, int64_t, int, int, const float *,
@@ -624,33 +619,6 @@ int pnr_latent_channels_last_backward(const float *g, float *const *d_maps, cons
         return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_backward: NULL");
     return launch_latent_cl_bwd(g, d_maps, channels, heights, widths, n_maps, n_images, out_h, out_w,
                                 (hipStream_t)stream);
-}
-
-size_t pnr_batchnorm_workspace_bytes(int64_t M, int32_t C) { return M < 1 || C < 4 ? 0 : bn_workspace_bytes(M, C); }
-
-int pnr_batchnorm_train_forward(const float *y, const float *idt, const float *gamma, const float *beta,
-                                float *running_mean, float *running_var, int64_t *num_batches_tracked, int64_t M,
-                                int32_t C, float momentum, float eps, int32_t relu, float *out, float *stats,
-                                void *ws, size_t ws_bytes, pnr_stream_t stream) {
-    if (!y || !gamma || !beta || !out || !stats) return fail(PNR_ERR_INVALID, "pnr_batchnorm_train_forward: NULL");
-    if ((running_mean == nullptr) != (running_var == nullptr))
-        return fail(PNR_ERR_INVALID, "pnr_batchnorm_train_forward: running_mean / running_var: both or neither");
-    if (((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(idt)) & 15) != 0)
-        return fail(PNR_ERR_INVALID, "pnr_batchnorm_train_forward: maps must be 16-byte aligned");
-    return launch_bn_forward(y, idt, gamma, beta, running_mean, running_var, num_batches_tracked, M, C, momentum, eps,
-                             relu, out, stats, ws, ws_bytes, (hipStream_t)stream);
-}
-
-int pnr_batchnorm_train_backward(const float *y, const float *out, const float *dout, const float *gamma,
-                                 const float *stats, int64_t M, int32_t C, int32_t relu, float *dy, float *d_idt,
-                                 float *d_gamma, float *d_beta, void *ws, size_t ws_bytes, pnr_stream_t stream) {
-    if (!y || !dout || !gamma || !stats || !dy || (relu && !out))
-        return fail(PNR_ERR_INVALID, "pnr_batchnorm_train_backward: NULL");
-    if (((reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(dout) |
-          reinterpret_cast<uintptr_t>(dy) | reinterpret_cast<uintptr_t>(d_idt)) & 15) != 0)
-        return fail(PNR_ERR_INVALID, "pnr_batchnorm_train_backward: maps must be 16-byte aligned");
-    return launch_bn_backward(y, out, dout, gamma, stats, M, C, relu, dy, d_idt, d_gamma, d_beta, ws, ws_bytes,
-                              (hipStream_t)stream);
 }
 
 int pnr_fold_batchnorm(const pnr_bn_fold *folds, int32_t n_folds, int64_t max_elems, pnr_stream_t stream) {

@@ -107,12 +107,7 @@ SIGNATURES = {
     "pnr_latent_channels_last_nhwc": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32),
                                               ctypes.POINTER(c_i32), c_i32, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "pnr_fold_batchnorm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
-    "pnr_batchnorm_workspace_bytes": (c_size, [c_i64, c_i32]),
     "pnr_latent_channels_last_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp]),
-    "pnr_batchnorm_train_forward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_f, c_f, c_i32,
-                                            c_vp, c_vp, c_vp, c_size, c_vp]),
-    "pnr_batchnorm_train_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_i32, c_i32, c_vp, c_vp, c_vp,
-                                             c_vp, c_vp, c_size, c_vp]),
     "pnr_point_save_floats": (c_size, [ctypes.POINTER(MlpDesc), c_i64]),
     "pnr_render_points": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp,
                                   ctypes.POINTER(Rays), c_vp, c_i32, c_vp, c_vp, c_vp, c_size, c_vp]),

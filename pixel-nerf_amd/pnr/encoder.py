@@ -11,7 +11,6 @@ per scene and is not part of the per-ray hot path.
 The hot path consumes the latent channels-LAST; ``latent_cl`` keeps that copy.
 """
 import ctypes
-import os
 import warnings
 import weakref
 
@@ -275,93 +274,6 @@ class InferenceTrunk:
         return out.clone()   # the graph's output buffer is rewritten by the next replay
 
 
-# per device: the BatchNorm kernels' workspaces, newest last.  Its arrival counters must be zero
-# before the first call and every call leaves them zero, so one zeroed buffer serves every call in
-# stream order; a grown one replaces it but the old stay allocated (a captured HIP graph may
-# still name them).
-_BN_WS = {}
-
-
-def _bn_workspace(y, c):
-    from . import _lib
-
-    nbytes = int(_lib.load().pnr_batchnorm_workspace_bytes(y.numel() // c, c))
-    held = _BN_WS.setdefault(y.device, [])
-    if not held or held[-1].numel() < nbytes:
-        held.append(torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=y.device))
-    return held[-1]
-
-
-class BatchNormTrain(torch.autograd.Function):
-    """[relu](batch_norm(y) [+ idt]) of a channels-last trunk map in training mode -- torch's
-    nn.BatchNorm2d on batch statistics (running statistics and num_batches_tracked updated as it
-    does) followed by BasicBlock's residual add and ReLU (encoder.py:135-149) -- as the
-    ``pnr_batchnorm_train_forward`` / ``_backward`` kernels (csrc/bn.hip): three launches each way
-    instead of MIOpen's three plus the add, relu and counter increments."""
-
-    @staticmethod
-    def forward(ctx, y, idt, weight, bias, bn, relu):
-        from . import _lib
-
-        c = y.shape[1]
-        out = torch.empty_like(y)
-        stats = torch.empty(2 * c, dtype=torch.float32, device=y.device)
-        ws = _bn_workspace(y, c)
-        rm, rv, nbt = (bn.running_mean, bn.running_var, bn.num_batches_tracked) if bn.track_running_stats else (
-            None, None, None)
-        _lib.check(_lib.load().pnr_batchnorm_train_forward(
-            _lib.ptr(y), _ptr(idt), _lib.ptr(weight), _lib.ptr(bias), _ptr(rm), _ptr(rv), _ptr(nbt),
-            y.numel() // c, c, float(bn.momentum), float(bn.eps), int(relu), _lib.ptr(out), _lib.ptr(stats),
-            _lib.ptr(ws), ws.numel(), _lib.stream_of(y.device)), "pnr_batchnorm_train_forward")
-        ctx.save_for_backward(y, out, weight, stats)
-        ctx.relu, ctx.has_idt = relu, idt is not None
-        return out
-
-    @staticmethod
-    def backward(ctx, g):
-        from . import _lib
-
-        y, out, weight, stats = ctx.saved_tensors
-        c = y.shape[1]
-        g = g.contiguous(memory_format=torch.channels_last)
-        dy = torch.empty_like(y)
-        didt = torch.empty_like(y) if ctx.has_idt and ctx.needs_input_grad[1] else None
-        dw = torch.empty(c, dtype=torch.float32, device=y.device)
-        db = torch.empty(c, dtype=torch.float32, device=y.device)
-        ws = _bn_workspace(y, c)
-        _lib.check(_lib.load().pnr_batchnorm_train_backward(
-            _lib.ptr(y), _lib.ptr(out), _lib.ptr(g), _lib.ptr(weight), _lib.ptr(stats), y.numel() // c, c,
-            int(ctx.relu), _lib.ptr(dy), _ptr(didt), _lib.ptr(dw), _lib.ptr(db), _lib.ptr(ws), ws.numel(),
-            _lib.stream_of(y.device)), "pnr_batchnorm_train_backward")
-        return dy, didt, dw, db, None, None
-
-
-# Train-mode BatchNorm(+add)(+relu) of the channels-last trunk through BatchNormTrain (csrc/bn.hip);
-# PNR_FUSED_BN=0: torch's nn.BatchNorm2d (MIOpen) + relu + add.
-FUSED_TRAIN_BN = os.environ.get("PNR_FUSED_BN", "1") != "0"
-
-
-def _fused_bn_ok(bn, y, idt):
-    """BatchNormTrain applies: plain affine BatchNorm2d in training mode with an exponential
-    momentum, an fp32 channels-last map on a HIP device, C a multiple of 4 dividing 1024."""
-    c = y.shape[1] if y.dim() == 4 else 0
-    return (FUSED_TRAIN_BN and type(bn) is nn.BatchNorm2d and bn.training and bn.affine and bn.momentum is not None
-            and y.is_cuda and y.dtype == torch.float32 and c >= 4 and c % 4 == 0 and 256 % (c // 4) == 0
-            and y.numel() > 0 and y.is_contiguous(memory_format=torch.channels_last) and bn.weight.dtype == torch.float32
-            and (idt is None or (idt.shape == y.shape and idt.dtype == y.dtype
-                                 and idt.is_contiguous(memory_format=torch.channels_last))))
-
-
-def bn_act(bn, y, relu=True, idt=None):
-    """[relu](bn(y) [+ idt]): the fused train-mode kernels where they apply, else torch's modules."""
-    if _fused_bn_ok(bn, y, idt):
-        return BatchNormTrain.apply(y, idt, bn.weight, bn.bias, bn, relu)
-    out = bn(y)
-    if idt is not None:
-        out = out + idt
-    return torch.relu(out) if relu else out
-
-
 class BasicBlock(nn.Module):
     expansion = 1
 
@@ -375,15 +287,10 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
 
     def forward(self, x):
-        if self.downsample is None:
-            idt = x
-        elif (isinstance(self.downsample, nn.Sequential) and len(self.downsample) == 2
-              and isinstance(self.downsample[1], nn.BatchNorm2d)):
-            idt = bn_act(self.downsample[1], self.downsample[0](x), relu=False)
-        else:
-            idt = self.downsample(x)
-        out = bn_act(self.bn1, self.conv1(x))
-        return bn_act(self.bn2, self.conv2(out), idt=idt)
+        idt = x if self.downsample is None else self.downsample(x)
+        out = self.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return self.relu(out + idt)
 
 
 class ResNetTrunk(nn.Module):
@@ -499,7 +406,7 @@ class SpatialEncoder(nn.Module):
         if self._use_infer(x):
             return self.set_latent_cl(self._infer.run(x))
         m = self.model
-        x = bn_act(m.bn1, m.conv1(x))
+        x = m.relu(m.bn1(m.conv1(x)))
         latents = [x]
         if self.num_layers > 1:
             if self.use_first_pool:
