@@ -66,14 +66,8 @@ __global__ __launch_bounds__(256) void k_merge_raw(const int *__restrict__ origi
 // One wave per ray, 4 rays per 256-thread block; the cumprod accumulates in double
 // (torch's CPU cumprod accumulates in double and rounds each prefix).
 // ---------------------------------------------------------------------------
-// K <= 256 (S = ceil(K / 64) chunks): lane l holds samples 64 i + l (i < S), so each load
-// instruction reads 1 KB of raw (and 256 B of z) contiguously; all loads issue before the first
-// wait (clamped addresses).  One exclusive double product scan per 64-sample chunk (DPP
-// row_shr / row_bcast / wave_shr, no LDS) with a running carry -- the association of the generic
-// k_composite -- then per-lane weight / colour sums and DPP wave reductions.  Measured against the
-// lane-owns-S-consecutive-samples layout (k_composite_s, tools/patches/composite_variants.diff):
-// 0.435-0.453 ms against 0.508-0.516 ms per 1 M rays x 128 without weights, 0.543-0.548 against
-// 0.551-0.560 with them (profiles/r5h, same box, alternating).
+// K <= 256: one wave per ray, lane l loads samples 64 i + l (1 KB of raw per load instruction),
+// all loads issued before the first wait (clamped addresses); composite_wave (march_dev.h).
 template <int S>
 __global__ __launch_bounds__(256) void k_composite_c(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
@@ -85,7 +79,7 @@ __global__ __launch_bounds__(256) void k_composite_c(
     const float far = rays[b * 8 + 7];
     const float *zr = z + b * K;
     const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
-    float zk[S];
+    float zk[S], wk[S];
     f4 v[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) {
@@ -94,51 +88,7 @@ __global__ __launch_bounds__(256) void k_composite_c(
         zk[i] = __builtin_nontemporal_load(zr + kc);
         v[i] = __builtin_nontemporal_load(rr + kc);
     }
-    double carry = 1.0;
-    float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const int k = 64 * i + lane;
-        const bool valid = k < K;
-        // the next sample's depth: lane + 1 of this chunk, or lane 0 of the next one for lane 63
-        const float nxt0 = i + 1 < S ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zk[i + 1 < S ? i + 1 : i]), 0))
-                                     : far;
-        // wave_shl:1, evaluated by every lane: under the select's branch the lane before the last
-        // valid one would read a disabled lane and keep `old`
-        const float zl = dpp_f<0x130>(nxt0, zk[i]);
-        const float zn = k + 1 >= K ? far : zl;
-        const float delta = sub_rn(zn, zk[i]);
-        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v[i].w, 0.0f)))) : 0.0f;
-        const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
-        const double incl = wave_scan_mul((double)shifted);
-        const double excl = wave_shr1(incl, 1.0);
-        const float wk = valid ? mul_rn(alpha, (float)(carry * excl)) : 0.f;
-        const long long il = __double_as_longlong(incl);
-        carry *= __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(il >> 32), 63) << 32) |
-                                      (unsigned)__builtin_amdgcn_readlane((int)il, 63));
-        if (weights && valid) __builtin_nontemporal_store(wk, weights + b * K + k);
-        sr += mul_rn(wk, v[i].x);
-        sg += mul_rn(wk, v[i].y);
-        sb += mul_rn(wk, v[i].z);
-        sd += mul_rn(wk, zk[i]);
-        sw += wk;
-    }
-    sr = wave_sum_dpp(sr);
-    sg = wave_sum_dpp(sg);
-    sb = wave_sum_dpp(sb);
-    sd = wave_sum_dpp(sd);
-    sw = wave_sum_dpp(sw);
-    if (lane == 0) {
-        if (white_bkgd) {
-            sr = sub_rn(add_rn(sr, 1.0f), sw);
-            sg = sub_rn(add_rn(sg, 1.0f), sw);
-            sb = sub_rn(add_rn(sb, 1.0f), sw);
-        }
-        rgb_out[b * 3 + 0] = sr;
-        rgb_out[b * 3 + 1] = sg;
-        rgb_out[b * 3 + 2] = sb;
-        depth_out[b] = sd;
-    }
+    composite_wave<S>(lane, b, K, far, zk, v, white_bkgd, weights, rgb_out, depth_out, wk);
 }
 
 // any K: 64-sample chunks, one wave scan per chunk with a running carry

@@ -12,7 +12,7 @@ out=$root/pixel-nerf_amd/build/$tag
 src=$out/src
 rm -rf "$out"; mkdir -p "$src/csrc" "$src/include"
 for f in march.hip mlp.hip train.hip encoder.hip bn.hip wgrad.hip proj.hip abi.cpp pnr_common.h march_dev.h pnr_diag.h; do
-  if [ "$rev" = WORKTREE ]; then cp "$root/pixel-nerf_amd/csrc/$f" "$src/csrc/$f"
+  if [ "$rev" = WORKTREE ]; then if [ -f "$root/pixel-nerf_amd/csrc/$f" ]; then cp "$root/pixel-nerf_amd/csrc/$f" "$src/csrc/$f"; fi
   else git -C "$root" show "$rev:pixel-nerf_amd/csrc/$f" > "$src/csrc/$f" 2>/dev/null || rm -f "$src/csrc/$f"; fi
 done
 if [ "$rev" = WORKTREE ]; then cp "$root/include/pnr_abi.h" "$src/include/"
