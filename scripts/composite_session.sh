@@ -4,7 +4,7 @@
 # tools/patches/composite_variants.diff); "default" is the tree's own.
 set -e
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-VARIANTS=${VARIANTS:-"default comps"}   # comps: PATCH=tools/patches/composite_variants.diff scripts/build_variant.sh comps WORKTREE
+VARIANTS=${VARIANTS:-"default compc"}   # compc: PATCH=tools/patches/composite_variants.diff scripts/build_variant.sh compc WORKTREE
 for t in $VARIANTS; do
   lib=pixel-nerf_amd/build/$t/libpnr.so; [ $t = default ] && lib=pixel-nerf_amd/pnr/libpnr.so
   echo "== check $t"; PNR_LIB_PATH=$lib timeout -k 10 120 python tools/composite_check.py 2>/dev/null | tail -12

@@ -1,8 +1,8 @@
 #!/bin/bash
 # Standalone composite kernel (bench.py composite_roofline: 1 M rays x 128 samples) for libpnr.so
 # variants, alternating: VARIANTS="default comp2" bash tools/composite_ab.sh.  The round-5 variants
-# (k_composite_s and its knobs) build from tools/patches/composite_variants.diff, e.g.
-#   PATCH=tools/patches/composite_variants.diff scripts/build_variant.sh comps WORKTREE
+# (the chunked layout) builds from tools/patches/composite_variants.diff, e.g.
+#   PATCH=tools/patches/composite_variants.diff scripts/build_variant.sh compc WORKTREE
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 for round in $(seq ${ROUNDS:-3}); do
   for t in ${VARIANTS:-default comp2}; do
