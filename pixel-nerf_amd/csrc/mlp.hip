@@ -363,7 +363,9 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
 #pragma unroll
         for (int r = 0; r < RTW; ++r) {
             const f4 v = acc[r][c];
+#ifndef PNR_ABLATE_SAVEF   // diagnostic (training results invalid): no fp32 save-slot stores
             *reinterpret_cast<f4 *>(slot + p * H + 16 * (RTW * wave + r) + 4 * g) = relu4(v);
+#endif
         }
     }
 }
@@ -383,9 +385,13 @@ __device__ __forceinline__ void save_mask(const Acc &acc, uint32_t *mslot, int64
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
         const uint32_t bits = nib(acc[0][c]) | (nib(acc[1][c]) << 4) | (nib(acc[2][c]) << 8) | (nib(acc[3][c]) << 12);
+#ifndef PNR_ABLATE_SAVEM   // diagnostic (training results invalid): no relu-mask stores
         if (p < n_points)
             *reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(mslot) + p * 64 + 8 * wave + 2 * g) =
                 (uint16_t)bits;
+#else
+        (void)bits;
+#endif
     }
 }
 

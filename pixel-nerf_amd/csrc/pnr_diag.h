@@ -24,6 +24,8 @@
 //                        permlane exchange (the stores and the column maxima stay).
 //   PNR_ABLATE_CMAXREAD  the relu publish takes constant column exponents: no column-maximum reads.
 //   PNR_ABLATE_BIAS      constants instead of bias loads.
+//   PNR_ABLATE_SAVEF     the training forward's fp32 activation-save stores (the relu slots) removed.
+//   PNR_ABLATE_SAVEM     the training forward's relu sign-mask stores removed.
 //   PNR_ABLATE_SPLIT     split-bf16 modes: the hi part only, no split VALU.
 //   PNR_ABLATE_STGREAD   split-bf16 modes: B operands from registers instead of the staging ring.
 //   PNR_ABLATE_KBARRIER  split-bf16 modes: no barrier between k-steps.
