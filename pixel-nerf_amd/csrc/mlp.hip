@@ -370,33 +370,27 @@ __device__ __forceinline__ void save_relu(const Acc &acc, float *slot, int64_t t
     }
 }
 
-typedef unsigned u2m __attribute__((ext_vector_type(2)));
-// [acc > 0] of this wave's rows -> mask slot, wave-major: the wave's 8-byte word of row q (q = row0
-// + point) at slot + 2 (wave PS + q) dwords.  Byte 2g + w of a word holds rows 16 (RTW wave + r) + 4g
-// + e, r = 2w + h, at bit 4h + e.  The four lanes of a column (g = 0..3, 16 apart) hold its four
-// 16-bit pieces; two lane shuffles gather them into lane g = 0, which stores the 8-byte word, so one
-// store instruction writes 16 consecutive points' words (128 contiguous bytes) -- a [point][64 B]
-// layout took one 2-byte store per lane, 16 cache lines per instruction (profiles/r5p: 0.7 ms of a
-// 15.7 ms forward at 786 k points).
-__device__ __forceinline__ void save_mask(const Acc &acc, uint32_t *mslot, int64_t PS, int64_t row0, int64_t tile,
-                                          int64_t n_points, int wave, int lane) {
+// [acc > 0] of this wave's rows -> mask slot [point][64 bytes].  Byte 8 wave + 2g + w of a
+// point holds rows 16 (RTW wave + r) + 4g + e, r = 2w + h, at bit 4h + e: a lane's 16 bits
+// are one contiguous 2-byte store per point, and a wave's 64 rows are one 8-byte word pair.
+__device__ __forceinline__ void save_mask(const Acc &acc, uint32_t *mslot, int64_t tile, int64_t n_points,
+                                          int wave, int lane) {
     static_assert(RTW == 4, "mask bytes assume 4 row tiles per wave");
     lane = opaque_lane(lane);
     const int g = lane >> 4, cl = lane & 15;
     auto nib = [](const f4 &v) {
         return (v.x > 0.f ? 1u : 0u) | (v.y > 0.f ? 2u : 0u) | (v.z > 0.f ? 4u : 0u) | (v.w > 0.f ? 8u : 0u);
     };
-    uint32_t *wbase = mslot + 2 * ((int64_t)wave * PS + row0);
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
         const uint32_t bits = nib(acc[0][c]) | (nib(acc[1][c]) << 4) | (nib(acc[2][c]) << 8) | (nib(acc[3][c]) << 12);
-        const uint32_t lo = bits | ((uint32_t)__shfl_down((int)bits, 16, 64) << 16);   // g = 0: b0 | b1, g = 2: b2 | b3
-        const uint32_t hi = (uint32_t)__shfl_down((int)lo, 32, 64);                     // g = 0: b2 | b3
 #ifndef PNR_ABLATE_SAVEM   // diagnostic (training results invalid): no relu-mask stores
-        if (g == 0 && p < n_points) *reinterpret_cast<u2m *>(wbase + 2 * p) = u2m{lo, hi};
+        if (p < n_points)
+            *reinterpret_cast<uint16_t *>(reinterpret_cast<char *>(mslot) + p * 64 + 8 * wave + 2 * g) =
+                (uint16_t)bits;
 #else
-        (void)hi;
+        (void)bits;
 #endif
     }
 }
@@ -1116,7 +1110,8 @@ __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const f
 template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // the activation save only in the training-forward instantiation (the ABI refuses a save with
-    // the projected latent or the march): the other kernels compile without its code
+    // the projected latent or the march): the render kernels compile without its code, which took
+    // the headline launch +0.5 % (profiles/r5q, same box)
     constexpr bool SAVE_OK = !PZ && !MARCH;
     constexpr int KD = H_DIST;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -1192,7 +1187,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
         if (SAVE_OK && a.save) {
             save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
-            save_mask(acc, sv_mask + PS * 16 * save_idx, PS, row0, tile, P, wave, lane);
+            save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
         }
 #ifdef PNR_GEMM_ONLY
         {   // diagnostic: GEMM chain only (garbage results); a checksum keeps acc live
@@ -1597,7 +1592,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             // activation save of lin_out's input remains
             if (SAVE_OK && a.save) {
                 save_relu(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
-                save_mask(x, sv_mask + PS * 16 * (2 * L.n_blocks), PS, 0, tile, P, wave, lane);
+                save_mask(x, sv_mask + PS * 16 * (2 * L.n_blocks), tile, P, wave, lane);
             }
         } else {
             publish_relu(x, tile, 2 * L.n_blocks, 0);
@@ -1781,15 +1776,15 @@ __device__ __forceinline__ void store_rows(const Acc &acc, float *slot, int64_t 
 }
 // relu backward masks from the forward's sign bits (save_mask): this lane's two words of
 // each of its CT points, loaded before the GEMM whose output they mask
-__device__ __forceinline__ void load_mask(u2m (&mk)[CT], const uint32_t *mslot, int64_t PS, int64_t row0,
-                                          int64_t tile, int64_t n_points, int wave, int lane) {
+typedef unsigned u2m __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void load_mask(u2m (&mk)[CT], const uint32_t *mslot, int64_t tile, int64_t n_points,
+                                          int wave, int lane) {
     const int cl = opaque_lane(lane) & 15;
-    const uint32_t *wbase = mslot + 2 * ((int64_t)wave * PS + row0);   // save_mask's wave-major words
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
         const int64_t p = tile * COLS + 16 * c + cl;
         const int64_t pc = p < n_points ? p : n_points - 1;
-        mk[c] = *reinterpret_cast<const u2m *>(wbase + 2 * pc);
+        mk[c] = *reinterpret_cast<const u2m *>(mslot + pc * 16 + 2 * wave);
     }
 }
 // acc *= [activation > 0] (torch's relu backward); 0 past n_points
@@ -1847,7 +1842,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     // relu sign masks of the forward: slot b: relu(x_b), nb + b: relu(h_b), 2 nb: x_f; every
     // region has PS rows (view rows v P + p before combine_layer)
     const uint32_t *msk = reinterpret_cast<const uint32_t *>(a.save + save_mask_offset(nb, PS));
-    auto mask_slot = [&](int i) { return msk + PS * 16 * i; };
+    auto mask_slot = [&](int i, int64_t row0) { return msk + PS * 16 * i + row0 * 16; };
     u2m mk[CT];
     auto dy_slot = [&](int i, int64_t row0) { return a.dy + PS * H * i + row0 * H; };
     auto bs_slot = [&](int i) -> float * {
@@ -1876,7 +1871,7 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
     for (int64_t tile = blockIdx.x; tile < a.n_tiles; tile += gridDim.x) {
         const bool first_tile = tile == blockIdx.x;
         {   // dx = (d_o W_out) . [x_f > 0]
-            load_mask(mk, mask_slot(2 * nb), PS, 0, tile, P, wave, lane);
+            load_mask(mk, mask_slot(2 * nb, 0), tile, P, wave, lane);
             f4 wo[4][RTW];
 #pragma unroll
             for (int j = 0; j < 4; ++j)
@@ -1923,13 +1918,13 @@ __global__ __launch_bounds__(NTHR) void k_mlp_bwd(BwdArgs a) {
                 store_rows(x, dy_slot(nb + 1 + b, row0), tile, P, wave, lane, bs_slot(nb + 1 + b), first);
                 const int l1 = layer_index(b, 2, L.n_linz), l0 = layer_index(b, 1, L.n_linz);
                 zero(h);
-                load_mask(mk, mask_slot(nb + b), PS, row0, tile, P, wave, lane);   // lands during the GEMM
+                load_mask(mk, mask_slot(nb + b, row0), tile, P, wave, lane);   // lands during the GEMM
                 layer_gemm<3, NKB, H_DIST, true>(h, layer(l1), gc, 1 + l1);
                 relu_mask(h, mk, tile, P, lane);
                 store_rows(h, dy_slot(b, row0), tile, P, wave, lane, bs_slot(b), first);
                 publish(h);
                 zero(h);
-                load_mask(mk, mask_slot(b), PS, row0, tile, P, wave, lane);
+                load_mask(mk, mask_slot(b, row0), tile, P, wave, lane);
                 layer_gemm<3, NKB, H_DIST, true>(h, layer(l0), gc, 1 + l0);
                 relu_mask(h, mk, tile, P, lane);
 #pragma unroll
