@@ -1109,10 +1109,6 @@ __device__ __forceinline__ void march_epilogue(const Args &a, int64_t b, const f
 // keeps its own register allocation
 template <int PREC, bool PZ, bool MARCH>
 __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
-    // the activation save only in the training-forward instantiation (the ABI refuses a save with
-    // the projected latent or the march): the render kernels compile without its code, which took
-    // the headline launch +0.5 % (profiles/r5q, same box)
-    constexpr bool SAVE_OK = !PZ && !MARCH;
     constexpr int KD = H_DIST;   // weight ring distance
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float *inbuf = smem;                   // COLS x LDS_LD
@@ -1185,7 +1181,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             lds_barrier();
     };
     auto publish_relu = [&](const Acc &acc, int64_t tile, int save_idx, int64_t row0) {
-        if (SAVE_OK && a.save) {
+        if (a.save) {
             save_relu(acc, sv_slot(save_idx) + row0 * H, tile, P, wave, lane);
             save_mask(acc, sv_mask + PS * 16 * save_idx + row0 * 16, tile, P, wave, lane);
         }
@@ -1367,7 +1363,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                     }
                     fv[i] = val;
                 }
-                if (SAVE_OK && a.save && p_raw < a.n_points) {
+                if (a.save && p_raw < a.n_points) {
 #pragma unroll
                     for (int i = 0; i < FPT / 4; ++i)
                         *reinterpret_cast<f4 *>(sv_f + (v * P + p_raw) * 64 + FPT * qt + 4 * i) =
@@ -1479,7 +1475,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                                   mul_rn(c2[q], tw.z)), mul_rn(c3[q], tw.w));
                         if constexpr (PREC == 3) zh[half] = zz;
                         else *reinterpret_cast<f4 *>(inbuf + cj * LDS_LD + ch) = zz;
-                        if (SAVE_OK && a.save && blk == 0 && tile * COLS + cj < P)
+                        if (a.save && blk == 0 && tile * COLS + cj < P)
                             *reinterpret_cast<f4 *>(sv_z + (v * P + tile * COLS + cj) * H + ch) = zz;
                     }
                     if constexpr (PREC == 3) {
@@ -1590,7 +1586,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         if constexpr (PREC == 3) {
             // no publish: the head reads relu(x) from the accumulators (below); only the
             // activation save of lin_out's input remains
-            if (SAVE_OK && a.save) {
+            if (a.save) {
                 save_relu(x, sv_slot(2 * L.n_blocks), tile, P, wave, lane);
                 save_mask(x, sv_mask + PS * 16 * (2 * L.n_blocks), tile, P, wave, lane);
             }
