@@ -129,10 +129,7 @@ __global__ __launch_bounds__(256) void k_composite_bwd(
 // corner per run of equal cells instead of per point.  The dL/dz chains of the run's
 // points are computed afterwards by lanes 0 .. RUN-1 in parallel.
 // ---------------------------------------------------------------------------
-#ifndef PNR_PIB_RUN
-#define PNR_PIB_RUN 8   // points per wave run (A/B knob)
-#endif
-constexpr int RUN = PNR_PIB_RUN;
+constexpr int RUN = 8;   // 4 and 16 measured slower on the cfg5 step (profiles/r5r)
 
 struct PointGeo {
     float xr[3], xc[3];
