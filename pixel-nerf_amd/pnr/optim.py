@@ -19,9 +19,12 @@ CHUNK = 8192   # elements per workgroup (a multiple of 4: chunk starts stay 16-B
 class Adam(torch.optim.Adam):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0, amsgrad=False, **kw):
         super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad, **kw)
-        self._pinned = None      # host staging of the chunk table
-        self._table = None       # device chunk table
-        self._copied = None      # event after the last table upload
+        # device chunk tables by (device, step run): rebuilt only when a pointer changes (the
+        # caching allocator normally hands the gradients the same blocks every step); an upload
+        # goes through a ring of pinned staging buffers, each reused only after its own copy
+        # event -- never a wait on the current step's work, which would stop the host running ahead
+        self._tables = {}
+        self._ring, self._ring_i = [], 0
 
     @staticmethod
     def _group_ok(group):
@@ -66,25 +69,39 @@ class Adam(torch.optim.Adam):
         n = np.array([p.numel() for p in ps], dtype=np.int64)
         ptr = np.array([(p.data_ptr(), p.grad.data_ptr(), self.state[p]["exp_avg"].data_ptr(),
                          self.state[p]["exp_avg_sq"].data_ptr()) for p in ps], dtype=np.int64).reshape(-1, 4)
-        nch = (n + CHUNK - 1) // CHUNK
-        total = int(nch.sum())
-        if total == 0:
-            return
-        idx = np.repeat(np.arange(len(ps)), nch)
-        off = (np.arange(total) - np.repeat(np.cumsum(nch) - nch, nch)) * CHUNK
-        rec = np.empty((total, 5), dtype=np.int64)   # include/pnr_abi.h pnr_adam_chunk: 4 pointers, n
-        rec[:, :4] = ptr[idx] + (off * 4)[:, None]
-        rec[:, 4] = np.minimum(CHUNK, n[idx] - off)
-        nbytes = rec.nbytes
-        if self._pinned is None or self._pinned.numel() < nbytes or self._table.device != dev:
-            self._pinned = torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True)
-            self._table = torch.empty(self._pinned.numel(), dtype=torch.uint8, device=dev)
-            self._copied = None
-        if self._copied is not None:
-            self._copied.synchronize()   # the previous upload read the staging buffer (long done)
-        self._pinned[:nbytes].numpy()[:] = np.frombuffer(rec.tobytes(), dtype=np.uint8)
-        self._table[:nbytes].copy_(self._pinned[:nbytes], non_blocking=True)
-        self._copied = torch.cuda.Event()
-        self._copied.record(torch.cuda.current_stream(dev))
-        _lib.check(_lib.load().pnr_adam_step(self._table.data_ptr(), total, lr, b1, b2, eps, wd, step,
+        key = (dev, ptr.tobytes(), n.tobytes())
+        tab = self._tables.get(dev)
+        if tab is None or tab[0] != key:
+            nch = (n + CHUNK - 1) // CHUNK
+            total = int(nch.sum())
+            if total == 0:
+                return
+            idx = np.repeat(np.arange(len(ps)), nch)
+            off = (np.arange(total) - np.repeat(np.cumsum(nch) - nch, nch)) * CHUNK
+            rec = np.empty((total, 5), dtype=np.int64)   # include/pnr_abi.h pnr_adam_chunk: 4 pointers, n
+            rec[:, :4] = ptr[idx] + (off * 4)[:, None]
+            rec[:, 4] = np.minimum(CHUNK, n[idx] - off)
+            raw = np.frombuffer(rec.tobytes(), dtype=np.uint8)
+            dev_tab = torch.empty(raw.size, dtype=torch.uint8, device=dev)
+            pinned, evt = self._stage(raw.size)
+            pinned[:raw.size].numpy()[:] = raw
+            dev_tab.copy_(pinned[:raw.size], non_blocking=True)
+            evt.record(torch.cuda.current_stream(dev))
+            tab = (key, dev_tab, total)
+            self._tables[dev] = tab
+        _lib.check(_lib.load().pnr_adam_step(tab[1].data_ptr(), tab[2], lr, b1, b2, eps, wd, step,
                                              _lib.stream_of(dev)), "pnr_adam_step")
+
+    def _stage(self, nbytes):
+        """A pinned staging buffer of the 4-slot ring, its previous upload finished."""
+        if len(self._ring) < 4:
+            self._ring.append([torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True), torch.cuda.Event()])
+            slot = self._ring[-1]
+        else:
+            slot = self._ring[self._ring_i]
+            self._ring_i = (self._ring_i + 1) % 4
+            slot[1].synchronize()
+            if slot[0].numel() < nbytes:
+                slot[0] = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        slot[1] = torch.cuda.Event()
+        return slot[0], slot[1]

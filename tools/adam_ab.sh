@@ -2,7 +2,7 @@
 # pnr.optim.Adam (one pnr_adam_step launch) against torch's fused Adam on the cfg5 step: the parity
 # test, then alternating scripts/bench_train.py runs with PNR_ADAM=pnr / torch.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -k adam -q --timeout 200 -p no:cacheprovider 2>&1 | tail -2
+timeout -k 10 300 python -u -m pytest tests/test_gpu_train.py -k adam -q --tb=short --timeout 200 -p no:cacheprovider 2>&1 | grep -E "^E |passed|failed|Error|test_gpu_train.py:[0-9]+" | head -30
 for round in 1 2 3; do
   for v in pnr torch; do
     echo -n "$round adam=$v: "
