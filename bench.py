@@ -451,10 +451,10 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
     pdist.set_batchnorm_mode(net.encoder, bn)
     net.train()
     renderer = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(dev)
-    # Adam (the reference's torch.optim.Adam, same update and state): pnr.optim.Adam, ONE
+    # Adam (the reference's torch.optim.Adam): torch's fused multi-tensor Adam; PNR_ADAM=pnr: pnr.optim.Adam, ONE
     # pnr_adam_step launch over every parameter; PNR_ADAM=torch (and the graph-replayed step, which
     # needs the device-side step counter of capturable) use torch's fused multi-tensor Adam
-    if graph or os.environ.get("PNR_ADAM", "pnr") == "torch":
+    if graph or os.environ.get("PNR_ADAM", "torch") == "torch":
         opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=graph)
     else:
         from pnr.optim import Adam as PnrAdam
