@@ -451,15 +451,9 @@ def train_leg(dev, rank, world, steps, warmup, precision="f16x3", sb=4, per=256,
     pdist.set_batchnorm_mode(net.encoder, bn)
     net.train()
     renderer = NeRFRenderer(n_coarse=64, n_fine=32, n_fine_depth=16, depth_std=0.01, white_bkgd=True).to(dev)
-    # Adam (the reference's torch.optim.Adam): torch's fused multi-tensor Adam (capturable in the
-    # graph-replayed step: a device-side step counter); PNR_ADAM=pnr: pnr.optim.Adam, ONE
-    # pnr_adam_step launch over every parameter (A/B, tools/adam_ab.sh)
-    if graph or os.environ.get("PNR_ADAM", "torch") == "torch":
-        opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=graph)
-    else:
-        from pnr.optim import Adam as PnrAdam
-
-        opt = PnrAdam(net.parameters(), lr=1e-4)
+    # fused Adam: one multi-tensor kernel per step (the reference uses torch.optim.Adam, same update);
+    # capturable keeps the step counter on the device so the update replays inside a graph
+    opt = torch.optim.Adam(net.parameters(), lr=1e-4, fused=True, capturable=graph)
     params = list(net.parameters())
     focal = torch.tensor(131.25, device=dev)
     src_poses = synth.srn_poses([float(15 * i + 7 * rank + 40 * v) for i in range(sb) for v in range(ns)]).to(dev)

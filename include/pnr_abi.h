@@ -34,7 +34,7 @@ extern "C" {
                                5: pnr_latent_channels_last_nhwc;
                                6: pnr_fold_batchnorm;
                                7: pnr_latent_channels_last_backward,
-                                  pnr_points_input_backward_masked, pnr_adam_step */
+                                  pnr_points_input_backward_masked */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -330,21 +330,6 @@ int pnr_latent_channels_last_nhwc(const float *const *maps, const int32_t *chann
 int pnr_latent_channels_last_backward(const float *g, float *const *d_maps, const int32_t *channels,
                                       const int32_t *heights, const int32_t *widths, int32_t n_maps,
                                       int32_t n_images, int32_t out_h, int32_t out_w, pnr_stream_t stream);
-
-/* Adam update of the training step (train.py's torch.optim.Adam): one
- * launch over `chunks` (DEVICE memory, n_chunks records; a record = up to a few thousand consecutive
- * elements of one fp32 tensor, its parameter / gradient / first / second moment pointers already
- * offset), per element g += wd p (wd != 0), m = b1 m + (1 - b1) g, v = b2 v + (1 - b2) g^2,
- * p -= lr / (1 - b1^step) m / (sqrt(v) / sqrt(1 - b2^step) + eps).  `step` >= 1 is the update's
- * count after this step (torch's state['step']).  pnr.optim.Adam (ABI 7). */
-typedef struct pnr_adam_chunk {
-    float *param;
-    const float *grad;
-    float *exp_avg, *exp_avg_sq;
-    int64_t n;
-} pnr_adam_chunk;
-int pnr_adam_step(const pnr_adam_chunk *chunks, int32_t n_chunks, float lr, float beta1, float beta2, float eps,
-                  float weight_decay, int64_t step, pnr_stream_t stream);
 
 /* One (convolution, BatchNorm) pair of the eval-mode encoder trunk (encoder.py:135-149 with the
  * BatchNorms on their running statistics).  conv_w / w_out: n_out blocks of per_out contiguous

@@ -35,7 +35,6 @@ size_t wgrad_workspace_bytes(int, int64_t);
 int launch_wgrad(const float *const *, const float *const *, float *const *, int, int64_t, void *, size_t,
                  hipStream_t, int arith);
 int launch_fold_bn(const pnr_bn_fold *, int, int64_t, hipStream_t);
-int launch_adam(const void *, int, float, float, float, float, float, int64_t, hipStream_t);
 int launch_latent_cl_bwd(const float *, float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, int,
                          int, hipStream_t);
 int launch_latent_cl(const float *const *, const int32_t *, const int32_t *, const int32_t *, int, int, float *,
@@ -620,12 +619,6 @@ int pnr_latent_channels_last_backward(const float *g, float *const *d_maps, cons
         return fail(PNR_ERR_INVALID, "pnr_latent_channels_last_backward: NULL");
     return launch_latent_cl_bwd(g, d_maps, channels, heights, widths, n_maps, n_images, out_h, out_w,
                                 (hipStream_t)stream);
-}
-
-int pnr_adam_step(const pnr_adam_chunk *chunks, int32_t n_chunks, float lr, float beta1, float beta2, float eps,
-                  float weight_decay, int64_t step, pnr_stream_t stream) {
-    static_assert(sizeof(pnr_adam_chunk) == 40, "pnr_adam_chunk layout");
-    return launch_adam(chunks, n_chunks, lr, beta1, beta2, eps, weight_decay, step, (hipStream_t)stream);
 }
 
 int pnr_fold_batchnorm(const pnr_bn_fold *folds, int32_t n_folds, int64_t max_elems, pnr_stream_t stream) {

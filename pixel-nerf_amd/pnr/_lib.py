@@ -107,7 +107,6 @@ SIGNATURES = {
     "pnr_latent_channels_last_nhwc": (c_i32, [ctypes.POINTER(c_vp), ctypes.POINTER(c_i32), ctypes.POINTER(c_i32),
                                               ctypes.POINTER(c_i32), c_i32, c_i32, c_vp, c_i32, c_i32, c_vp]),
     "pnr_fold_batchnorm": (c_i32, [c_vp, c_i32, c_i64, c_vp]),
-    "pnr_adam_step": (c_i32, [c_vp, c_i32, c_f, c_f, c_f, c_f, c_f, c_i64, c_vp]),
     "pnr_latent_channels_last_backward": (c_i32, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i32, c_i32, c_i32, c_i32, c_vp]),
     "pnr_point_save_floats": (c_size, [ctypes.POINTER(MlpDesc), c_i64]),
     "pnr_render_points": (c_i32, [ctypes.POINTER(Scene), ctypes.POINTER(MlpDesc), c_vp,

@@ -11,7 +11,7 @@ root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/pixel-nerf_amd/build/$tag
 src=$out/src
 rm -rf "$out"; mkdir -p "$src/csrc" "$src/include"
-for f in march.hip mlp.hip train.hip encoder.hip bn.hip optim.hip wgrad.hip proj.hip abi.cpp pnr_common.h march_dev.h pnr_diag.h; do
+for f in march.hip mlp.hip train.hip encoder.hip bn.hip wgrad.hip proj.hip abi.cpp pnr_common.h march_dev.h pnr_diag.h; do
   if [ "$rev" = WORKTREE ]; then if [ -f "$root/pixel-nerf_amd/csrc/$f" ]; then cp "$root/pixel-nerf_amd/csrc/$f" "$src/csrc/$f"; fi
   else git -C "$root" show "$rev:pixel-nerf_amd/csrc/$f" > "$src/csrc/$f" 2>/dev/null || rm -f "$src/csrc/$f"; fi
 done
@@ -24,7 +24,7 @@ fi
 # sources include "../../include/pnr_abi.h" relative to csrc/
 mkdir -p "$out/include"; cp "$src/include/pnr_abi.h" "$out/include/"
 objs=()
-for f in march.hip mlp.hip train.hip encoder.hip bn.hip optim.hip wgrad.hip proj.hip abi.cpp; do
+for f in march.hip mlp.hip train.hip encoder.hip bn.hip wgrad.hip proj.hip abi.cpp; do
   [ -f "$src/csrc/$f" ] || continue   # older revisions lack later files
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w "$@" -I"$src/csrc" \
     -x hip -c "$src/csrc/$f" -o "$out/$f.o" &

@@ -39,8 +39,6 @@ def test_abi_version_and_error_channel():
     assert lib.pnr_fold_batchnorm(None, 3, 10, None) == -1 and b"NULL" in lib.pnr_last_error()
     assert lib.pnr_latent_channels_last_backward(None, None, None, None, None, 1, 1, 4, 4, None) == -1
     assert b"NULL" in lib.pnr_last_error()
-    assert lib.pnr_adam_step(None, 3, 1e-3, 0.9, 0.999, 1e-8, 0.0, 1, None) == -1 and b"NULL" in lib.pnr_last_error()
-    assert lib.pnr_adam_step(None, 0, 1e-3, 0.9, 0.999, 1e-8, 0.0, 0, None) == -1 and b"step" in lib.pnr_last_error()
     # an invalid call fails with a message, without touching the GPU
     rc = lib.pnr_composite(None, None, None, 4, 0, 0, None, None, None, None)
     assert rc == -1
@@ -417,23 +415,3 @@ def test_encoder_forward_matches_reference_fixture_cpu():
         torch.testing.assert_close(enc.latent_scaling, torch.from_numpy(g["latent_scaling_%d" % i]))
         if c["train"]:
             torch.testing.assert_close(enc.model.bn1.running_mean, torch.from_numpy(g["running_mean_after_%d" % i]))
-
-
-def test_pnr_adam_on_cpu_is_torch_adam():
-    """pnr.optim.Adam keeps torch.optim.Adam's algorithm, state and state_dict; CPU parameters step
-    through torch's own implementation (the HIP launch covers fp32 device tensors)."""
-    from pnr.optim import Adam as PnrAdam
-
-    g = torch.Generator().manual_seed(0)
-    a = [torch.randn(5, 3, generator=g).requires_grad_(True), torch.randn(7, generator=g).requires_grad_(True)]
-    b = [t.detach().clone().requires_grad_(True) for t in a]
-    oa, ob = PnrAdam(a, lr=1e-2, weight_decay=0.1), torch.optim.Adam(b, lr=1e-2, weight_decay=0.1)
-    for _ in range(3):
-        for pa, pb in zip(a, b):
-            gr = torch.randn(pa.shape, generator=g)
-            pa.grad, pb.grad = gr, gr.clone()
-        oa.step()
-        ob.step()
-    for pa, pb in zip(a, b):
-        assert torch.equal(pa, pb)
-    assert oa.state_dict()["state"].keys() == ob.state_dict()["state"].keys()
