@@ -88,7 +88,9 @@ __global__ __launch_bounds__(256) void k_composite_s(
         far[j] = rays[b * 8 + 7];
         const float *zr = z + b * K;
         const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
-        if (S == 2 && (K & 1) == 0) {   // 8-B aligned pair of depths
+        // the pair as one 8-B load when it is 8-B aligned: K even and z itself 8-B aligned (a caller
+        // may pass a view at an odd float offset, pnr_composite: ADVICE r5)
+        if (S == 2 && (K & 1) == 0 && (reinterpret_cast<uintptr_t>(z) & 7) == 0) {
             typedef float f2 __attribute__((ext_vector_type(2)));
             const int kc = k0 < K ? k0 : K - 2;
             const f2 zz = __builtin_nontemporal_load(reinterpret_cast<const f2 *>(zr + kc));

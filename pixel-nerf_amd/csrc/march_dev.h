@@ -77,7 +77,7 @@ __device__ __forceinline__ float composite_wave(int lane, int64_t b, int K, floa
     }
     if (weights) {
         float *wp = weights + b * K + k0;
-        if (S == 2 && (K & 1) == 0 && k0 < K) {   // 8-B aligned pair
+        if (S == 2 && (K & 1) == 0 && k0 < K && (reinterpret_cast<uintptr_t>(weights) & 7) == 0) {   // 8-B aligned pair
             typedef float f2 __attribute__((ext_vector_type(2)));
             __builtin_nontemporal_store(f2{wk[0], wk[1]}, reinterpret_cast<f2 *>(wp));
         } else {

@@ -1037,6 +1037,30 @@ __device__ __forceinline__ void layer_gemm(Acc &acc, const float *layer_base, Ge
     PT(g, 2);
 }
 
+// One lane's global atomic add of 1 to *p; the old value is returned to every lane.  The lane mask
+// is narrowed and restored inside the asm, so the caller is straight-line code with no divergent
+// region.  (The tile claim was `if (tid == 0) *s_next = grab();`: ROCm 7.2's register allocator
+// placed a spill of the thread id in that branch's join block BEFORE its EXEC restore, so only
+// lane 0 stored it and every other lane reloaded stale scratch -- the round-5 illegal-address
+// faults.  isa_lint.py now rejects any build with a spill in that position.)  Called by a whole
+// wave with every lane active, so lane 0 is the lane that adds.
+__device__ __forceinline__ int claim_one(int *p) {
+    int old;
+    unsigned long long saved;
+    asm volatile(
+        "s_mov_b64 %1, exec\n\t"
+        "s_mov_b64 exec, 1\n\t"
+        "s_nop 4\n\t"
+        "global_atomic_add %0, %2, %3, off sc0\n\t"
+        "s_mov_b64 exec, %1\n\t"
+        "s_waitcnt vmcnt(0)\n\t"
+        "s_nop 4"
+        : "=&v"(old), "=&s"(saved)
+        : "v"(p), "v"(1)
+        : "memory");
+    return __builtin_amdgcn_readfirstlane(old);
+}
+
 // The march config read where it is used (kernarg s_loads through a pointer the compiler cannot
 // see through): hoisted out of the tile loop, its ~30 loop-invariant dwords held SGPRs across
 // the GEMMs and spilled them (256 SGPR spills, 40 B/lane of VGPR scratch against 16).
@@ -1138,7 +1162,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // PE freqs [0, 16) / phases [16, 32) of the pack header, in LDS: the feature loop indexes
     // them per lane, and vector global loads there put a memory latency in every iteration
     float *petab = PREC == 3 ? reinterpret_cast<float *>(ecol + COLS) : gtab + COLS * 8;
-    if (tid < 32) petab[tid] = a.packed[tid];   // visible after the first barrier of a tile
+    // (the one-time LDS fills below are whole-wave writes -- lanes 32 apart store the same value --
+    // rather than `if (tid < 32)` branches: no divergent region for a misplaced spill, claim_one)
+    if (wave == 0) petab[lane & 31] = a.packed[lane & 31];   // visible after the first barrier of a tile
     gc.hdr = a.packed;
     // B fragment (column 16c + cl, k 32 ks + 8g): swz keeps it linear in ks and c
     gc.pb0 = P0 + cl * ROWH + swz(cl, 8 * g);
@@ -1150,7 +1176,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     gc.fair.mate = 0;
     if constexpr (PREC == 3) {
         gc.fair.prog = reinterpret_cast<int *>(petab + 40);   // petab + 32 / 33: s_next, + 64: hpart
-        if (tid < WAVES) gc.fair.prog[tid] = 0;   // visible after the first barrier
+        if (wave == 0) gc.fair.prog[lane & (WAVES - 1)] = 0;   // visible after the first barrier
     }
     gc.wave = wave;
     gc.lane = lane;
@@ -1243,7 +1269,8 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
     // single launch: the fine tiles' PE table from the fine pack's header (the packs
     // of two MLPs may carry different tables); visible after the first barrier
     float *petab_f = mnf + 4;
-    if (single && tid >= 64 && tid < 96) petab_f[tid - 64] = march_cfg(a)->packed_f[tid - 64];
+    if (single && wave == 1) petab_f[lane & 31] = march_cfg(a)->packed_f[lane & 31];
+    // the next unit's first tile, claimed by wave 0 (wave-uniform: every value here is scalar)
     auto grab = [&]() -> int {
         const int64_t T = a.n_tiles / upt;
         const int x0 = blockIdx.x & 7;
@@ -1251,12 +1278,12 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             const int x = (x0 + k) & 7;
             const int64_t lo = x * T / 8, hi = (x + 1) * T / 8;
             if (lo >= hi) continue;
-            const int64_t i = lo + atomicAdd(a.tile_ctr + 16 * x, 1);
+            const int64_t i = lo + claim_one(a.tile_ctr + 16 * x);
             if (i < hi) return (int)(i * upt);
         }
         return (int)a.n_tiles;
     };
-    if (tid == 0) *s_next = grab();
+    if (wave == 0) *s_next = grab();
     lds_barrier();
     for (int64_t tile = *s_next; tile < a.n_tiles; tile = *s_next) {
         // this tile within its unit: pass_f = a fine tile of the single-launch march; sub = the
@@ -1581,7 +1608,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                                       PREC == 3 ? &R1 : nullptr);
         }
         // ---- lin_out(relu(x)) + head [sigmoid(rgb), relu(sigma)]: wave w < CT -> columns 16w..
-        if (tid == 0) *s_next = s_in + 1 < upt ? tile + 1 : grab();   // read after the closing barrier
+        if (wave == 0) *s_next = s_in + 1 < upt ? (int)tile + 1 : grab();   // read after the closing barrier
         pre_publish_sync();
         if constexpr (PREC == 3) {
             // no publish: the head reads relu(x) from the accumulators (below); only the

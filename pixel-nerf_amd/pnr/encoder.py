@@ -109,6 +109,17 @@ def _ptr(t):
     return None if t is None else t.data_ptr()
 
 
+def _bn_foldable(module):
+    """Every BatchNorm of ``module`` (itself included) is affine and tracks running statistics: the
+    fold (k_fold_bn) reads all four tensors, and an eval-mode BatchNorm without running statistics
+    normalizes by the batch's, which no fold represents -- such an encoder runs the module path."""
+    for b in module.modules():
+        if isinstance(b, nn.modules.batchnorm._BatchNorm) and (
+                b.running_mean is None or b.running_var is None or b.weight is None or b.bias is None):
+            return False
+    return True
+
+
 class InferenceTrunk:
     """The encoder trunk for rendering (eval mode, no autograd; encoder.py:135-164's forward with
     the BatchNorms on their running statistics, what gen_video.py / eval.py run after .eval()):
@@ -161,6 +172,9 @@ class InferenceTrunk:
         if key == self.key:
             return
         for i, (c, b) in enumerate(pairs):
+            if not _bn_foldable(b):   # k_fold_bn reads mean / var / weight / bias
+                raise ValueError("pnr: the folded trunk needs every BatchNorm2d affine with running "
+                                 "statistics (%r)" % (b,))
             w = c.weight
             if w.dtype != torch.float32 or w.device != self.device or not (
                     w.is_contiguous() or w.is_contiguous(memory_format=torch.channels_last)):
@@ -436,7 +450,7 @@ class SpatialEncoder(nn.Module):
         bilinear channels-last latent."""
         if not (self.infer_fast and x.is_cuda and not self.training and not torch.is_grad_enabled()
                 and self.upsample_interp == "bilinear" and isinstance(self.model.bn1, nn.BatchNorm2d)
-                and self.model.bn1.track_running_stats):
+                and _bn_foldable(self.model)):
             return False
         if self._infer is None or self._infer.device != x.device or self._infer.owner() is not self:
             self._infer = InferenceTrunk(self, x.device)

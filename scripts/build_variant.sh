@@ -26,11 +26,22 @@ mkdir -p "$out/include"; cp "$src/include/pnr_abi.h" "$out/include/"
 objs=()
 for f in march.hip mlp.hip train.hip encoder.hip bn.hip wgrad.hip proj.hip abi.cpp; do
   [ -f "$src/csrc/$f" ] || continue   # older revisions lack later files
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w "$@" -I"$src/csrc" \
-    -x hip -c "$src/csrc/$f" -o "$out/$f.o" &
+  mkdir -p "$out/tmp_$f"
+  # -save-temps=obj: the device assembly for isa_lint.py (the Makefile's check)
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -w "$@" -I"$src/csrc" -save-temps=obj \
+    -x hip -c "$src/csrc/$f" -o "$out/tmp_$f/$f.o" &
   objs+=("$out/$f.o")
 done
 wait
+for f in march.hip mlp.hip train.hip encoder.hip bn.hip wgrad.hip proj.hip abi.cpp; do
+  [ -f "$src/csrc/$f" ] || continue
+  mv "$out/tmp_$f/$f.o" "$out/$f.o"
+  mv "$out/tmp_$f/"*-hip-amdgcn-amd-amdhsa-gfx950.s "$out/$f.gfx950.s"
+  rm -rf "$out/tmp_$f"
+done
+# a variant that would hand stale scratch to masked lanes never reaches the GPU (LINT=0: only to
+# reproduce the round-5 fault deliberately)
+if [ "${LINT:-1}" != 0 ]; then python3 "$root/pixel-nerf_amd/isa_lint.py" "$out"/*.gfx950.s; fi
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out/libpnr.so" "${objs[@]}" -Wl,-soname,libpnr.so \
   -Wl,-rpath,/opt/rocm/lib
 echo "built $out/libpnr.so"

@@ -39,9 +39,19 @@ def extra_args(ap):
     ap.add_argument("--no_bbox_step", type=int, default=100000, help="Step to stop using bbox sampling")
     ap.add_argument("--fixed_test", action="store_true", default=None, help="accepted; unused (as in train.py)")
     ap.add_argument("--max_steps", type=int, default=None, help="stop after this many steps (then save)")
-    ap.add_argument("--image_size", type=int, default=128, help="SRN loader image size")
+    ap.add_argument("--image_size", type=int, default=None,
+                    help="resample every image to this square size (default: the loader's own -- SRN 128, "
+                         "DVR NMR / DTU and multi-object their native size, as train.py passes none)")
     ap.add_argument("--seed", type=int, default=0)
     return ap
+
+
+def load_datasets(fmt, datadir, image_size=None):
+    """train.py:74's get_split_dataset(args.dataset_format, args.datadir): the loaders' own image
+    size unless --image_size is given (train.py passes none, so ShapeNet-NMR stays 64 x 64 and DTU
+    300 x 400 with their own intrinsics; MultiObjectDataset takes no size at all)."""
+    kw = {} if image_size is None else {"image_size": (image_size, image_size)}
+    return get_split_dataset(fmt, datadir, **kw)
 
 
 def main(argv=None):
@@ -60,8 +70,7 @@ def main(argv=None):
     torch.cuda.set_device(device)
     seed_everything(args.seed + rank)
 
-    dset, val_dset, _ = get_split_dataset(args.dataset_format, args.datadir,
-                                          image_size=(args.image_size, args.image_size))
+    dset, val_dset, _ = load_datasets(args.dataset_format, args.datadir, args.image_size)
     net = make_model(conf["model"]).to(device=device)
     net.stop_encoder_grad = args.freeze_enc
     if args.freeze_enc:

@@ -437,3 +437,33 @@ def test_color_jitter_is_the_tensor_colour_transform():
     y = (bri * y).clamp(0, 1)
     torch.testing.assert_close(out[0], y * 2 - 1, atol=1e-6, rtol=0)
     assert float(out.min()) >= -1 and float(out.max()) <= 1
+
+
+@pytest.mark.parametrize("fmt,tag", [("dvr", "nmr"), ("dvr_dtu", "dtu")])
+def test_train_script_keeps_the_loader_image_size(tmp_path, fmt, tag):
+    """scripts/train.py: without --image_size the DVR loaders run at their native size
+    with their own intrinsics, as train.py:74 calls get_split_dataset with no size; the items equal
+    the reference loader's on the same directory (tests/golden/dvr_loader.npz)."""
+    import importlib.util
+    import os
+
+    import dvr_synth
+
+    spec = importlib.util.spec_from_file_location(
+        "pnr_train_script", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts",
+                                         "train.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    g = _dvr_golden()
+    prefix = "new_" if tag == "dtu" else "softras_"
+    for st in ("train", "val", "test"):
+        root = dvr_synth.write_dvr_dir(str(tmp_path), _dvr_inputs(g, tag), list_prefix=prefix, stage=st)
+    tr, va, te = mod.load_datasets(fmt, root)
+    base = tr.base_dset if hasattr(tr, "base_dset") else tr
+    item = te[0]
+    assert tuple(item["images"].shape[-2:]) == tuple(g["%s_0_images" % tag].shape[-2:])
+    _check_item(item, g, "%s_0_" % tag, atol=2e-5 if tag == "dtu" else 1e-6)   # images, focal, c, poses
+    assert base.image_size is None
+    # an explicit --image_size still resamples
+    _, _, te2 = mod.load_datasets(fmt, root, 10)
+    assert tuple(te2[0]["images"].shape[-2:]) == (10, 10)

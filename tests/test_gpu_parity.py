@@ -119,6 +119,50 @@ def test_composite_empty_batch():
     assert rgb.shape == (0, 3) and d.shape == (0,)
 
 
+def test_composite_unaligned_z_and_weights_through_the_abi():
+    """pnr_composite with z and weights at an odd float offset (a view into a larger buffer): the
+    paired 8-B depth load / weight store is only taken for 8-B-aligned pointers, so
+    the results are bit-identical to the aligned call; raw must be 16-B aligned and is refused
+    otherwise."""
+    import ctypes
+
+    from pnr import _lib
+
+    def at(t, off=0):
+        return ctypes.c_void_p(t.data_ptr() + off)
+
+    g = torch.Generator().manual_seed(5)
+    B, K = 67, 128   # K in (64, 128]: the S = 2 kernel
+    rays = torch.cat([torch.randn(B, 6, generator=g), torch.full((B, 1), 0.3), torch.full((B, 1), 4.0)], 1).to(DEV)
+    z = torch.sort(0.3 + 3.7 * torch.rand(B, K, generator=g), -1)[0].to(DEV)
+    raw = torch.rand(B, K, 4, generator=g)
+    raw[..., 3] = torch.randn(B, K, generator=g) * 4.0
+    raw = raw.to(DEV)
+    lib = _lib.load()
+    st = _lib.stream_of(torch.device(DEV))
+
+    def run(zp, wp):
+        rgb = torch.empty(B, 3, device=DEV)
+        d = torch.empty(B, device=DEV)
+        _lib.check(lib.pnr_composite(zp, at(raw), at(rays), B, K, 1, wp, at(rgb), at(d), st), "pnr_composite")
+        return rgb, d
+
+    w0 = torch.empty(B, K, device=DEV)
+    rgb0, d0 = run(at(z), at(w0))
+    zbuf = torch.empty(B * K + 1, device=DEV)
+    zbuf[1:] = z.reshape(-1)
+    wbuf = torch.zeros(B * K + 1, device=DEV)
+    rgb1, d1 = run(at(zbuf, 4), at(wbuf, 4))
+    torch.cuda.synchronize()
+    assert torch.equal(rgb0, rgb1) and torch.equal(d0, d1)
+    assert torch.equal(w0.reshape(-1), wbuf[1:]) and float(wbuf[0]) == 0.0
+    rgb_ref = ref_cpu.composite(rays.cpu(), z.cpu(), raw.cpu(), True)[1]
+    assert_close(rgb1, rgb_ref, "rgb (unaligned)")
+    rawbuf = torch.empty(B * K * 4 + 1, device=DEV)
+    rc = lib.pnr_composite(at(z), at(rawbuf, 4), at(rays), B, K, 1, None, at(rgb0), at(d0), st)
+    assert rc != 0
+
+
 @pytest.mark.parametrize("lindisp", [False, True])
 def test_sample_coarse_matches_oracle(lindisp):
     g = torch.Generator().manual_seed(1)

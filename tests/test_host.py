@@ -340,6 +340,88 @@ def test_inference_trunk_fold_table_follows_the_module():
     assert enc._infer is None
 
 
+def test_inference_trunk_refuses_batchnorm_without_running_stats():
+    """a BatchNorm with track_running_stats=False (running_mean / running_var None) or
+    affine=False has no tensors for k_fold_bn to read, and in eval mode normalizes by the batch's
+    statistics, which no fold represents: such an encoder takes the module path (_use_infer is
+    False on any device), and the trunk itself raises instead of handing the kernel NULL."""
+    from pnr.encoder import InferenceTrunk, SpatialEncoder, _bn_foldable
+
+    enc = SpatialEncoder(pretrained=False).eval()
+    assert _bn_foldable(enc.model)
+    for bad in (torch.nn.BatchNorm2d(128, track_running_stats=False), torch.nn.BatchNorm2d(128, affine=False)):
+        enc.model.layer2[1].bn2 = bad
+        assert not _bn_foldable(enc.model)
+        with pytest.raises(ValueError, match="running"):
+            InferenceTrunk(enc, torch.device("cpu")).refresh()
+        with torch.no_grad():   # the module path still encodes (on the CPU here)
+            assert torch.isfinite(enc(torch.rand(1, 3, 32, 32))).all()
+
+
+_LINT_BAD = """\
+_ZN3pnr4mlpk11k_point_mlpILi6ELb1ELb1EEEvNS0_4ArgsE:
+\tv_mov_b32_e32 v5, v0
+\tv_cmp_eq_u32_e64 s[10:11], 0, v5
+\ts_mov_b64 s[6:7], exec
+\ts_and_b64 s[10:11], s[6:7], s[10:11]
+\ts_mov_b64 exec, s[10:11]
+\ts_cbranch_execz .LBB12_21
+; %bb.7:
+\tglobal_atomic_add v3, v0, v3, s[24:25] sc0
+.LBB12_21:
+\ts_mov_b32 s20, s34
+\tscratch_store_dword off, v5, off offset:4 ; 4-byte Folded Spill
+\ts_or_b64 exec, exec, s[6:7]
+\ts_barrier
+\tscratch_load_dword v49, off, off offset:4 ; 4-byte Folded Reload
+.Lfunc_end12:
+"""
+
+
+def test_isa_lint_flags_a_spill_under_a_branch_mask(tmp_path):
+    """pixel-nerf_amd/isa_lint.py (the build's check): the round-5 fault pattern --
+    k_point_mlp<6,true,true> of the 8299515 tree spilled the thread id in the join block of
+    `if (tid == 0)` before the EXEC restore -- is rejected; the same spill after the restore, or a
+    spill inside a region (after its own EXEC write), is not."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("isa_lint", os.path.join(REPO, "pixel-nerf_amd", "isa_lint.py"))
+    lint = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lint)
+    bad = tmp_path / "bad.s"
+    bad.write_text(_LINT_BAD)
+    hits = lint.lint_file(str(bad))
+    assert len(hits) == 1 and "offset:4" in hits[0][2] and hits[0][0].endswith("ArgsE")
+    assert lint.main([str(bad)]) == 1
+    good = tmp_path / "good.s"
+    good.write_text(_LINT_BAD.replace("\tscratch_store_dword off, v5, off offset:4 ; 4-byte Folded Spill\n"
+                                      "\ts_or_b64 exec, exec, s[6:7]\n",
+                                      "\ts_or_b64 exec, exec, s[6:7]\n"
+                                      "\tscratch_store_dword off, v5, off offset:4 ; 4-byte Folded Spill\n"))
+    assert lint.lint_file(str(good)) == [] and lint.main([str(good)]) == 0
+    inside = tmp_path / "inside.s"   # a reload inside the region: its own mask write comes first
+    inside.write_text(_LINT_BAD.replace("\ts_mov_b32 s20, s34\n", "\ts_and_saveexec_b64 s[8:9], vcc\n"))
+    assert lint.lint_file(str(inside)) == []
+
+
+def test_built_device_code_passes_isa_lint():
+    """Every device object of the in-tree build (the Makefile keeps each one's assembly as
+    build/<source>.gfx950.s) is free of spills under a branch's lane mask."""
+    import glob
+    import importlib.util
+
+    files = sorted(glob.glob(os.path.join(REPO, "pixel-nerf_amd", "build", "*.gfx950.s")))
+    if not files:
+        pytest.skip("no in-tree build (make -C pixel-nerf_amd)")
+    names = {os.path.basename(f) for f in files}
+    assert {"mlp.hip.gfx950.s", "march.hip.gfx950.s", "train.hip.gfx950.s", "wgrad.hip.gfx950.s"} <= names
+    spec = importlib.util.spec_from_file_location("isa_lint", os.path.join(REPO, "pixel-nerf_amd", "isa_lint.py"))
+    lint = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lint)
+    for f in files:
+        assert lint.lint_file(f) == [], f
+
+
 def _torchvision_resnet34_keys():
     """torchvision.models.resnet34's state-dict names and shapes (BasicBlock x [3, 4, 6, 3],
     widths 64 / 128 / 256 / 512, a 1x1-conv + BatchNorm downsample on the first block of layers
