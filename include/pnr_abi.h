@@ -283,7 +283,7 @@ int pnr_sample_fine(const float *rays, int64_t n_rays, int32_t n_coarse,
  * z (n_rays, K), raw (n_rays, K, 4) = model output [r, g, b, sigma];
  * weights (n_rays, K) may be NULL; rgb (n_rays, 3); depth (n_rays).
  * raw must be 16-byte aligned (PNR_ERR_INVALID otherwise); z and weights need only float
- * alignment (an 8-byte-aligned z / weights takes the paired load / store). */
+ * alignment. */
 int pnr_composite(const float *z, const float *raw, const float *rays, int64_t n_rays,
                   int32_t k, int32_t white_bkgd, float *weights, float *rgb, float *depth,
                   pnr_stream_t stream);

@@ -66,53 +66,29 @@ __global__ __launch_bounds__(256) void k_merge_raw(const int *__restrict__ origi
 // One wave per ray, 4 rays per 256-thread block; the cumprod accumulates in double
 // (torch's CPU cumprod accumulates in double and rounds each prefix).
 // ---------------------------------------------------------------------------
-// S > 0 (K <= 64 S): lane l owns the S consecutive samples 64-lane-contiguous at S*l:
-// one sequential double product inside the lane, then ONE exclusive wave scan of the
-// lane products per ray; the next sample's z comes from the neighbour lane by shuffle.
+// K <= 256: one wave per ray, lane l loads samples 64 i + l (1 KB of raw per load instruction),
+// all loads issued before the first wait (clamped addresses); composite_wave (march_dev.h).
 template <int S>
-__global__ __launch_bounds__(256) void k_composite_s(
+__global__ __launch_bounds__(256) void k_composite_c(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
     int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
     float *__restrict__ rgb_out, float *__restrict__ depth_out) {
-    constexpr int RPW = 1;   // rays per wave (2 and 4 measured no faster: tools/patches/composite_variants.diff)
     const int lane = threadIdx.x & 63;
-    const int64_t b0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
-    if (b0 >= n_rays) return;
-    const int k0 = S * lane;
-    float zk[RPW][S], far[RPW];
-    f4 v[RPW][S];
-    // unconditional (clamped) loads: every ray's loads issue before the first wait
+    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (b >= n_rays) return;
+    const float far = rays[b * 8 + 7];
+    const float *zr = z + b * K;
+    const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
+    float zk[S], wk[S];
+    f4 v[S];
 #pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        const int64_t b = b0 + j < n_rays ? b0 + j : n_rays - 1;
-        far[j] = rays[b * 8 + 7];
-        const float *zr = z + b * K;
-        const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
-        // the pair as one 8-B load when it is 8-B aligned: K even and z itself 8-B aligned (a caller
-        // may pass a view at an odd float offset, pnr_composite: ADVICE r5)
-        if (S == 2 && (K & 1) == 0 && (reinterpret_cast<uintptr_t>(z) & 7) == 0) {
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            const int kc = k0 < K ? k0 : K - 2;
-            const f2 zz = __builtin_nontemporal_load(reinterpret_cast<const f2 *>(zr + kc));
-            zk[j][0] = zz.x;
-            zk[j][S - 1] = zz.y;
-#pragma unroll
-            for (int i = 0; i < S; ++i) v[j][i] = __builtin_nontemporal_load(rr + kc + i);
-        } else {
-#pragma unroll
-            for (int i = 0; i < S; ++i) {
-                const int kc = k0 + i < K ? k0 + i : K - 1;
-                zk[j][i] = __builtin_nontemporal_load(zr + kc);
-                v[j][i] = __builtin_nontemporal_load(rr + kc);
-            }
-        }
+    for (int i = 0; i < S; ++i) {
+        const int k = 64 * i + lane;
+        const int kc = k < K ? k : K - 1;
+        zk[i] = __builtin_nontemporal_load(zr + kc);
+        v[i] = __builtin_nontemporal_load(rr + kc);
     }
-#pragma unroll
-    for (int j = 0; j < RPW; ++j) {
-        if (b0 + j >= n_rays) break;
-        float wk[S];
-        composite_wave<S>(lane, b0 + j, K, far[j], zk[j], v[j], white_bkgd, weights, rgb_out, depth_out, wk);
-    }
+    composite_wave<S>(lane, b, K, far, zk, v, white_bkgd, weights, rgb_out, depth_out, wk);
 }
 
 // any K: 64-sample chunks, one wave scan per chunk with a running carry
@@ -258,8 +234,8 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
     if (n_rays == 0) return PNR_OK;
     const int nch = (K + 63) / 64;
     const int64_t grid = (n_rays + 3) / 4;   // one wave per ray
-    auto kern = nch == 1 ? k_composite_s<1> : nch == 2 ? k_composite_s<2> : nch == 3 ? k_composite_s<3>
-              : nch == 4 ? k_composite_s<4> : k_composite;
+    auto kern = nch == 1 ? k_composite_c<1> : nch == 2 ? k_composite_c<2> : nch == 3 ? k_composite_c<3>
+              : nch == 4 ? k_composite_c<4> : k_composite;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, st, z, raw, rays,
                        n_rays, K, white_bkgd, weights, rgb, depth);
     return launch_ok("composite") ? PNR_OK : PNR_ERR_HIP;

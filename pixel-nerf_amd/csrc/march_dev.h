@@ -39,52 +39,47 @@ __device__ __forceinline__ float coarse_z(const RngSrc &u, int64_t b, int kc, in
 //   delta_i = z_{i+1} - z_i, delta_last = far - z_last
 //   alpha = 1 - exp(-delta * relu(sigma));  T = excl. cumprod(1 - alpha + 1e-10)
 //   w = alpha * T;  rgb = sum w c;  depth = sum w z;  white: rgb += 1 - sum w
-// K <= 64 S: lane l holds the S consecutive samples S*l .. S*l+S-1 (zk, v; lanes past K hold
-// clamped copies).  One sequential double product inside the lane, then ONE exclusive wave
-// scan of the lane products (torch's CPU cumprod accumulates in double and rounds each
-// prefix); the next sample's z comes from the neighbour lane by DPP.  Writes the weights
-// (if non-NULL), rgb and depth of ray b; returns the weights in wk and the depth (every lane).
+// K <= 64 S (S = ceil(K / 64) chunks): lane l holds samples 64 i + l of chunk i (zk, v; lanes past
+// K hold clamped copies), so a ray's loads are lane-contiguous (1 KB of raw per instruction from
+// HBM, conflict-free from LDS).  One exclusive double product scan per chunk (torch's CPU cumprod
+// accumulates in double and rounds each prefix) with a running carry; the next sample's z comes
+// from the neighbour lane by DPP (lane 63: lane 0 of the next chunk).  Writes the weights (if
+// non-NULL), rgb and depth of ray b; returns the weights in wk and the depth (every lane).  The
+// standalone composite and the fused march's epilogue both run this, so the unfused march is
+// bit-identical to the fused one.  (Round 4's layout -- lane l owning the S consecutive samples
+// S l .. -- measured 12-16 % slower standalone: tools/patches/composite_variants.diff, profiles/r6b.)
 template <int S>
 __device__ __forceinline__ float composite_wave(int lane, int64_t b, int K, float far, const float (&zk)[S],
                                                 const f4 (&v)[S], int white_bkgd, float *weights,
                                                 float *rgb_out, float *depth_out, float (&wk)[S]) {
-    const int k0 = S * lane;
-    const float z_next_lane = dpp_f<0x130>(far, zk[0]);   // wave_shl:1 (lane + 1)
-    float alpha[S];
-    double lp[S + 1];   // exclusive in-lane prefix products
-    lp[0] = 1.0;
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const int k = k0 + i;
-        const bool valid = k < K;
-        const float zn = k + 1 >= K ? far : (i + 1 < S ? zk[i + 1] : z_next_lane);
-        const float delta = sub_rn(zn, zk[i]);
-        alpha[i] = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v[i].w, 0.0f)))) : 0.0f;
-        const float shifted = valid ? add_rn(sub_rn(1.0f, alpha[i]), 1e-10f) : 1.0f;
-        lp[i + 1] = lp[i] * (double)shifted;
-    }
-    const double excl = wave_shr1(wave_scan_mul(lp[S]), 1.0);   // product of earlier lanes
+    double carry = 1.0;
     float sr = 0.f, sg = 0.f, sb = 0.f, sd = 0.f, sw = 0.f;
 #pragma unroll
     for (int i = 0; i < S; ++i) {
-        const bool valid = k0 + i < K;
-        wk[i] = valid ? mul_rn(alpha[i], (float)(excl * lp[i])) : 0.f;
+        const int k = 64 * i + lane;
+        const bool valid = k < K;
+        // the next sample's depth: lane + 1 of this chunk, or lane 0 of the next one for lane 63
+        const float nxt0 = i + 1 < S ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(zk[i + 1 < S ? i + 1 : i]), 0))
+                                     : far;
+        // wave_shl:1, evaluated by every lane: inside the select below the compiler issues it
+        // under a branch, and the lane before the last valid sample then reads a disabled lane
+        const float zl = dpp_f<0x130>(nxt0, zk[i]);
+        const float zn = k + 1 >= K ? far : zl;
+        const float delta = sub_rn(zn, zk[i]);
+        const float alpha = valid ? sub_rn(1.0f, expf(mul_rn(-delta, max_nc(v[i].w, 0.0f)))) : 0.0f;
+        const float shifted = valid ? add_rn(sub_rn(1.0f, alpha), 1e-10f) : 1.0f;
+        const double incl = wave_scan_mul((double)shifted);
+        const double excl = wave_shr1(incl, 1.0);
+        wk[i] = valid ? mul_rn(alpha, (float)(carry * excl)) : 0.f;
+        const long long il = __double_as_longlong(incl);
+        carry *= __longlong_as_double(((long long)__builtin_amdgcn_readlane((int)(il >> 32), 63) << 32) |
+                                      (unsigned)__builtin_amdgcn_readlane((int)il, 63));
+        if (weights && valid) __builtin_nontemporal_store(wk[i], weights + b * K + k);
         sr += mul_rn(wk[i], v[i].x);
         sg += mul_rn(wk[i], v[i].y);
         sb += mul_rn(wk[i], v[i].z);
         sd += mul_rn(wk[i], zk[i]);
         sw += wk[i];
-    }
-    if (weights) {
-        float *wp = weights + b * K + k0;
-        if (S == 2 && (K & 1) == 0 && k0 < K && (reinterpret_cast<uintptr_t>(weights) & 7) == 0) {   // 8-B aligned pair
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            __builtin_nontemporal_store(f2{wk[0], wk[1]}, reinterpret_cast<f2 *>(wp));
-        } else {
-#pragma unroll
-            for (int i = 0; i < S; ++i)
-                if (k0 + i < K) __builtin_nontemporal_store(wk[i], wp + i);
-        }
     }
     sr = wave_sum_dpp(sr);
     sg = wave_sum_dpp(sg);

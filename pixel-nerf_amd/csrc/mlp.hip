@@ -1099,9 +1099,9 @@ __device__ __forceinline__ void march_ray(const Args &a, int64_t b, const float 
     float zk[S], wk[S];
     f4 v[S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
-        zk[i] = buf[S * lane + i];
-        v[i] = *reinterpret_cast<const f4 *>(buf + 128 + 4 * (S * lane + i));
+    for (int i = 0; i < S; ++i) {   // composite_wave's lane ownership: sample 64 i + lane
+        zk[i] = buf[64 * i + lane];
+        v[i] = *reinterpret_cast<const f4 *>(buf + 128 + 4 * (64 * i + lane));
     }
     const float depth = fine_pass
         ? composite_wave<S>(lane, b, COLS * S, far, zk, v, c->white_bkgd, c->weights_f, c->rgb_f, c->depth_f, wk)
@@ -1113,7 +1113,7 @@ __device__ __forceinline__ void march_ray(const Args &a, int64_t b, const float 
     if (kf > 0) {
         float *w = scr;
 #pragma unroll
-        for (int i = 0; i < S; ++i) w[S * lane + i] = wk[i];
+        for (int i = 0; i < S; ++i) w[64 * i + lane] = wk[i];
         wave_lds_sync();
         // single launch: the sorted fine depths also go to buf's z region (whose coarse depths
         // composite_wave and the sort's inputs have consumed) for the ray's fine tiles
