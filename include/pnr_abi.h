@@ -30,11 +30,12 @@
 extern "C" {
 #endif
 
-#define PNR_ABI_VERSION 7   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
+#define PNR_ABI_VERSION 8   /* 4: pnr_weight_grad_arith (per-call weight-gradient arithmetic);
                                5: pnr_latent_channels_last_nhwc;
                                6: pnr_fold_batchnorm;
                                7: pnr_latent_channels_last_backward,
-                                  pnr_points_input_backward_masked */
+                                  pnr_points_input_backward_masked;
+                               8: pnr_render_cfg.ray_order */
 
 typedef enum pnr_status {
     PNR_OK = 0,
@@ -145,6 +146,13 @@ typedef struct pnr_render_cfg {
      *  -1  the process default set by pnr_render_set_fused (initially 2).
      * All modes give bit-identical results. */
     int32_t march_mode;
+    /* ABI 8: the order in which the fused march (modes 1-3) takes the rays, or NULL (input
+     * order).  ray_order[i] is the index of the i-th ray to process; it should be a permutation
+     * of 0 .. n_rays - 1 (an entry out of range processes ray i instead).  Every draw and every
+     * output stays at the ray's own index, so the results are bit-identical to NULL's; only the
+     * schedule -- which rays share an XCD's L2 at a time -- changes (NeRFRenderer.ray_order:
+     * pixel blocks of 16 x 16 rays). */
+    const int32_t *ray_order;
 } pnr_render_cfg;
 
 /* Outputs; any pointer may be NULL except the rgb/depth of each pass that runs. */

@@ -433,6 +433,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
                         sort_width(kall) <= 128 && coarse_proj && fine_proj;
     if (single) {
         MarchCfg m = {};
+        m.order = cfg->ray_order;
         m.kpt = 1;
         m.sample_coarse = 1;
         m.lindisp = cfg->lindisp;
@@ -470,6 +471,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     if ((rc = mark(0))) return rc;
     if (fuse_c) {
         MarchCfg m = {};
+        m.order = cfg->ray_order;
         m.kpt = kc / 64;
         m.sample_coarse = 1;
         m.lindisp = cfg->lindisp;
@@ -517,6 +519,7 @@ int pnr_render_forward_proj(const pnr_scene *scene, const pnr_mlp_desc *desc, co
     if ((rc = mark(4))) return rc;
     if (fuse_f) {
         MarchCfg m = {};
+        m.order = cfg->ray_order;
         m.kpt = kall / 64;
         m.white_bkgd = cfg->white_bkgd;
         m.weights = out->fine_weights;

@@ -66,29 +66,40 @@ __global__ __launch_bounds__(256) void k_merge_raw(const int *__restrict__ origi
 // One wave per ray, 4 rays per 256-thread block; the cumprod accumulates in double
 // (torch's CPU cumprod accumulates in double and rounds each prefix).
 // ---------------------------------------------------------------------------
-// K <= 256: one wave per ray, lane l loads samples 64 i + l (1 KB of raw per load instruction),
-// all loads issued before the first wait (clamped addresses); composite_wave (march_dev.h).
+// K <= 256: one wave per two rays, lane l loads samples 64 i + l of both (1 KB of raw per load
+// instruction), all loads issued before the first wait (clamped addresses), then composite_wave
+// (march_dev.h) per ray.  Two rays per wave: +6-8 % over one (0.78-0.79 against 0.72-0.73 of HBM
+// peak, same box, profiles/r6e/ab_rpw2.txt): twice the bytes in flight per wave.
 template <int S>
 __global__ __launch_bounds__(256) void k_composite_c(
     const float *__restrict__ z, const float *__restrict__ raw, const float *__restrict__ rays,
     int64_t n_rays, int K, int white_bkgd, float *__restrict__ weights,
     float *__restrict__ rgb_out, float *__restrict__ depth_out) {
+    constexpr int RPW = 2;   // rays per wave
     const int lane = threadIdx.x & 63;
-    const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (b >= n_rays) return;
-    const float far = rays[b * 8 + 7];
-    const float *zr = z + b * K;
-    const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
-    float zk[S], wk[S];
-    f4 v[S];
+    const int64_t b0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+    if (b0 >= n_rays) return;
+    float zk[RPW][S], wk[S], far[RPW];
+    f4 v[RPW][S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
-        const int k = 64 * i + lane;
-        const int kc = k < K ? k : K - 1;
-        zk[i] = __builtin_nontemporal_load(zr + kc);
-        v[i] = __builtin_nontemporal_load(rr + kc);
+    for (int j = 0; j < RPW; ++j) {
+        const int64_t b = b0 + j < n_rays ? b0 + j : n_rays - 1;
+        far[j] = rays[b * 8 + 7];
+        const float *zr = z + b * K;
+        const f4 *rr = reinterpret_cast<const f4 *>(raw) + b * K;
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+            const int k = 64 * i + lane;
+            const int kc = k < K ? k : K - 1;
+            zk[j][i] = __builtin_nontemporal_load(zr + kc);
+            v[j][i] = __builtin_nontemporal_load(rr + kc);
+        }
     }
-    composite_wave<S>(lane, b, K, far, zk, v, white_bkgd, weights, rgb_out, depth_out, wk);
+#pragma unroll
+    for (int j = 0; j < RPW; ++j) {
+        if (b0 + j >= n_rays) break;
+        composite_wave<S>(lane, b0 + j, K, far[j], zk[j], v[j], white_bkgd, weights, rgb_out, depth_out, wk);
+    }
 }
 
 // any K: 64-sample chunks, one wave scan per chunk with a running carry
@@ -233,7 +244,7 @@ int launch_composite(const float *z, const float *raw, const float *rays, int64_
                      int white_bkgd, float *weights, float *rgb, float *depth, hipStream_t st) {
     if (n_rays == 0) return PNR_OK;
     const int nch = (K + 63) / 64;
-    const int64_t grid = (n_rays + 3) / 4;   // one wave per ray
+    const int64_t grid = (n_rays + 7) / 8;   // one wave per two rays
     auto kern = nch == 1 ? k_composite_c<1> : nch == 2 ? k_composite_c<2> : nch == 3 ? k_composite_c<3>
               : nch == 4 ? k_composite_c<4> : k_composite;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), 0, st, z, raw, rays,

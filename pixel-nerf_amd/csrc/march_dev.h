@@ -304,6 +304,9 @@ struct MarchCfg {
     int single, kpt_f;
     const float *packed_f, *proj_f;          // the fine MLP's pack and projected latent
     float *weights_f, *rgb_f, *depth_f;      // fine composite outputs (weights_f may be NULL)
+    // processing order (pnr_render_cfg.ray_order): scheduling unit i marches ray order[i]; NULL =
+    // unit i is ray i.  Draws and outputs use the ray's own index, so results do not depend on it.
+    const int *order;
 };
 // LDS floats of the fused march region (k_point_mlp): the ray's z (128) | raw (128 x 4), the
 // epilogue scratch w (128) | cdf (128) | sort (128), near / far (4), and with the single-launch

@@ -1293,6 +1293,14 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
         const bool pass_f = single && s_in >= kpt;
         const int sub = pass_f ? s_in - kpt : s_in;
         const int kpt_t = pass_f ? march_cfg(a)->kpt_f : kpt;
+        // MARCH: the unit's ray (pnr_render_cfg.ray_order; read at use, an L2-hit scalar load);
+        // an entry out of range marches the unit's own index instead of faulting
+        auto ray_of = [&]() -> int64_t {
+            const int *o = MARCH ? march_cfg(a)->order : nullptr;
+            if (!o) return unit;
+            const int64_t r = o[unit];
+            return r >= 0 && r < a.n_tiles / upt ? r : unit;
+        };
         // the pass's pack and projected latent (read at use: no per-tile SGPR state)
         auto PK = [&]() -> const float * { return pass_f ? march_cfg(a)->packed_f : a.packed; };
         auto PJ_ = [&]() -> const float * { return pass_f ? march_cfg(a)->proj_f : a.proj; };
@@ -1315,7 +1323,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             int64_t obj;
             if (a.render_mode) {
                 // ray b, sample kk of its pass (MARCH: the unit's ray, K = 64 kpt_t)
-                const int64_t b = MARCH ? unit : p / a.K;
+                const int64_t b = MARCH ? ray_of() : p / a.K;
                 const int kk = MARCH ? sub * COLS + col : (int)(p - b * a.K);
                 const int kt = MARCH ? COLS * kpt_t : a.K;
                 const float *ray = a.rays + b * 8;
@@ -1366,7 +1374,7 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
             if (MARCH && qt == 0 && v == 0) {   // for the epilogue
                 if (!pass_f) mreg[sub * COLS + col] = zz;
                 if (col == 0 && sub == 0) {
-                    const float *rr = a.rays + unit * 8;
+                    const float *rr = a.rays + ray_of() * 8;
                     mnf[0] = rr[6];
                     mnf[1] = rr[7];
                 }
@@ -1680,7 +1688,9 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
                 r.w = max_nc(o.w, 0.f);   // torch.relu: NaN stays NaN
-                if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+                if (!MARCH || a.out)   // MARCH: the ray's own points (ray_order)
+                    *reinterpret_cast<f4 *>(a.out + (MARCH ? ray_of() * (COLS * kpt_t) + sub * COLS + 16 * wave + cl
+                                                           : po) * 4) = r;
                 if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * (sub * COLS + 16 * wave + cl)) = r;
             }
         }
@@ -1702,14 +1712,15 @@ __global__ __launch_bounds__(NTHR) void k_point_mlp(Args a) {
                 r.y = __fdiv_rn(1.f, add_rn(1.f, expf(-o.y)));
                 r.z = __fdiv_rn(1.f, add_rn(1.f, expf(-o.z)));
                 r.w = max_nc(o.w, 0.f);   // torch.relu: NaN stays NaN
-                if (!MARCH || a.out) *reinterpret_cast<f4 *>(a.out + po * 4) = r;
+                if (!MARCH || a.out)   // MARCH: the ray's own points (ray_order)
+                    *reinterpret_cast<f4 *>(a.out + (MARCH ? ray_of() * (COLS * kpt_t) + sub * COLS + col : po) * 4) = r;
                 if (MARCH) *reinterpret_cast<f4 *>(mreg + 128 + 4 * (sub * COLS + 16 * wave + cc)) = r;
             }
         }
         // ---- fused march: the ray's last tile composites it (and draws its fine samples) --
         if (MARCH && sub == kpt_t - 1) {   // the ray's last tile of this pass
             lds_barrier();   // the ray's head outputs visible
-            if (wave == WAVES - 1) march_epilogue(a, unit, mreg, mnf, mscr, opaque_lane(lane), pass_f);
+            if (wave == WAVES - 1) march_epilogue(a, ray_of(), mreg, mnf, mscr, opaque_lane(lane), pass_f);
         }
     }
 #ifdef PNR_PHASE_TIMING

@@ -103,7 +103,8 @@ std::vector<at::Tensor> render_rays(const at::Tensor &latent_cl, const at::Tenso
                                     const c10::optional<at::Tensor> &u_coarse, const c10::optional<at::Tensor> &u_fine,
                                     const c10::optional<at::Tensor> &u_fine_jit,
                                     const c10::optional<at::Tensor> &n_depth, int64_t seed, int64_t offset,
-                                    bool want_weights, bool want_z, at::IntArrayRef events, int64_t march_mode) {
+                                    bool want_weights, bool want_z, at::IntArrayRef events, int64_t march_mode,
+                                    const c10::optional<at::Tensor> &ray_order) {
     TORCH_CHECK(rays.dim() == 2 && rays.size(1) == 8, "rays must be (B, 8)");
     TORCH_CHECK(events.empty() || events.size() == 7, "events: none or 7 hipEvent_t handles");
     const at::Device dev = rays.device();
@@ -148,7 +149,14 @@ std::vector<at::Tensor> render_rays(const at::Tensor &latent_cl, const at::Tenso
     rng.seed = (uint64_t)seed;
     rng.offset = (uint64_t)offset;
     pnr_render_cfg cfg{(int32_t)n_coarse, (int32_t)n_fine, (int32_t)n_fine_depth, (float)depth_std,
-                       (int32_t)white_bkgd, (int32_t)lindisp, (int32_t)march_mode};
+                       (int32_t)white_bkgd, (int32_t)lindisp, (int32_t)march_mode, nullptr};
+    if (ray_order.has_value() && ray_order->defined()) {   // ABI 8: the march's processing order
+        const at::Tensor &ro = *ray_order;
+        same_device(ro, dev, "ray_order");
+        TORCH_CHECK(ro.scalar_type() == at::kInt && ro.dim() == 1 && ro.size(0) == B && ro.is_contiguous(),
+                    "ray_order must be a contiguous int32 (B,) tensor");
+        cfg.ray_order = ro.data_ptr<int32_t>();
+    }
     const size_t ws_bytes = pnr_render_workspace_bytes(&sc, &cfg, B);
     at::Tensor ws = at::empty({(int64_t)(ws_bytes ? ws_bytes : 1)}, rays.options().dtype(at::kByte));
     void *ev[7] = {};
@@ -173,7 +181,7 @@ std::vector<at::Tensor> render_rays_meta(const at::Tensor &latent_cl, const at::
                                          const c10::optional<at::Tensor> &u_fine_jit,
                                          const c10::optional<at::Tensor> &n_depth, int64_t seed, int64_t offset,
                                          bool want_weights, bool want_z, at::IntArrayRef events,
-                                         int64_t march_mode) {
+                                         int64_t march_mode, const c10::optional<at::Tensor> &ray_order) {
     const int64_t B = rays.size(0);
     const auto o = f32_like(rays);
     const bool fine = n_fine > 0;
@@ -250,7 +258,8 @@ TORCH_LIBRARY(pnr, m) {
           "int[] desc, Tensor coarse_packed, Tensor fine_packed, Tensor? coarse_proj, Tensor? fine_proj, "
           "Tensor rays, int rays_per_obj, int n_coarse, int n_fine, int n_fine_depth, float depth_std, "
           "bool white_bkgd, bool lindisp, Tensor? u_coarse, Tensor? u_fine, Tensor? u_fine_jit, Tensor? n_depth, "
-          "int seed, int offset, bool want_weights, bool want_z, int[] events=[], int march_mode=-1) -> Tensor[]");
+          "int seed, int offset, bool want_weights, bool want_z, int[] events=[], int march_mode=-1, "
+          "Tensor? ray_order=None) -> Tensor[]");
     m.def("point_query(Tensor latent_cl, Tensor cams, int n_obj, int n_views, float image_w, float image_h, "
           "int[] desc, Tensor packed, Tensor? proj, Tensor xyz, Tensor? viewdirs) -> Tensor");
     m.def("composite(Tensor z, Tensor raw, Tensor rays, bool white_bkgd, bool want_weights) -> Tensor[]");

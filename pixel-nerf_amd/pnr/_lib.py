@@ -54,13 +54,14 @@ class Rng(ctypes.Structure):
 
 # pnr_rng counter-mode stream ids (PNR_RNG_*)
 RNG_U_COARSE, RNG_U_FINE, RNG_U_FINE_JIT, RNG_N_DEPTH = 0, 1, 2, 3
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class RenderCfg(ctypes.Structure):
     _fields_ = [("n_coarse", c_i32), ("n_fine", c_i32), ("n_fine_depth", c_i32),
                 ("depth_std", c_f), ("white_bkgd", c_i32), ("lindisp", c_i32),
-                ("march_mode", c_i32)]   # ABI 3: -1 = the pnr_render_set_fused default
+                ("march_mode", c_i32),   # ABI 3: -1 = the pnr_render_set_fused default
+                ("ray_order", c_vp)]     # ABI 8: the fused march's processing order (NULL: input order)
 
 
 class RenderOut(ctypes.Structure):

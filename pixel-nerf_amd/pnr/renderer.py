@@ -64,6 +64,54 @@ class _RenderWrapper(torch.nn.Module):
         return outputs.toDict()
 
 
+# ray_order "auto": block the rays when the projected latent rows (views x H_l x W_l x 2 KB x lin_z
+# stages) exceed this -- past the XCDs' L2s and a good part of the 256 MB Infinity Cache
+ORDER_AUTO_BYTES = 128 << 20
+
+
+def ray_block_order(rays, block=16):
+    """A processing order for a pinhole ray batch (pnr_render_cfg.ray_order): rays grouped in
+    block x block squares of neighbouring pixels, the squares row by row, the input order kept
+    inside a square.  Rays sharing a square sample neighbouring latent pixels in every source
+    view, so the scheduling units running at once on an XCD share its L2 (cfg4).
+    The target camera is not known here: the image plane is the plane perpendicular to the mean
+    direction, at unit distance, and the pixel rows' direction and pitch the median step between
+    consecutive rays (one pixel along a row for row-major input, gen_video's / eval's frames).  Returns an int32 (B,) permutation, or None when the rays
+    do not look like one pinhole camera's (then the input order is kept)."""
+    B = rays.shape[0]
+    if B < 4 * block * block:
+        return None
+    o, d = rays[:, :3], rays[:, 3:6]
+    if float((o - o[:1]).abs().max()) > 1e-4 * (1.0 + float(o[0].abs().max())):
+        return None   # not one centre of projection
+    axis = d.mean(0)
+    axis = axis / axis.norm()
+    cz = d @ axis
+    if float(cz.min()) <= 1e-3:
+        return None
+    up = torch.zeros(3, device=d.device, dtype=d.dtype)
+    up[int(torch.argmin(axis.abs()))] = 1.0
+    e1 = torch.linalg.cross(axis, up)
+    e1 = e1 / e1.norm()
+    e2 = torch.linalg.cross(axis, e1)
+    t = d / cz[:, None]
+    u, v = t @ e1, t @ e2
+    # the pixel rows' direction and pitch: the median step between consecutive rays (one pixel
+    # along a row for row-major input; the row wraps are outliers), so the blocks align with
+    # the image's rows and columns
+    du, dv = float(torch.diff(u).median()), float(torch.diff(v).median())
+    pitch = (du * du + dv * dv) ** 0.5
+    if not pitch > 0.0:
+        return None
+    r1 = (e1 * du + e2 * dv) / pitch
+    r2 = torch.linalg.cross(axis, r1)
+    u, v = t @ r1, t @ r2
+    cu = torch.floor((u - u.min()) / (block * pitch)).long()
+    cv = torch.floor((v - v.min()) / (block * pitch)).long()
+    key = cv * (int(cu.max()) + 1) + cu
+    return torch.argsort(key, stable=True).to(torch.int32)
+
+
 class NeRFRenderer(torch.nn.Module):
     """NeRF volume renderer (nerf.py:45-371)."""
 
@@ -100,6 +148,12 @@ class NeRFRenderer(torch.nn.Module):
         # None = the library default (pnr_render_set_fused, initially 2), else 0, 1, 2 or 3; all
         # give bit-identical results; per call, so renderers in different threads may differ
         self.march_mode = None
+        # the fused march's processing order (pnr_render_cfg.ray_order, ABI 8; results are
+        # bit-identical in every order): "auto" = 16 x 16 blocks of neighbouring rays when the
+        # scene's projected-latent rows outgrow the caches (ORDER_AUTO_BYTES; cfg4's 3 views x
+        # 150 x 200 x 3 stages = 553 MB: -3.5 % frame time, profiles/r6c), else the input order;
+        # "blocked" / "input" force one
+        self.ray_order = "auto"
 
     # ---- random streams (nerf.py:111, 135, 141, 158) ---------------------------------
     def fine_counts(self):
@@ -312,12 +366,13 @@ class NeRFRenderer(torch.nn.Module):
             u_c = u_f = u_j = n_d = None
         else:
             u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
+        order = ray_block_order(rays) if sb == 1 and self._blocked_order(net) else None
         res = ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, pf, zc, zf, rays,
                                B // sb, kc, kf, kfd, float(self.depth_std), bool(self.white_bkgd),
                                bool(self.lindisp), u_c, u_f, u_j, n_d, int(seed or 0), int(offset),
                                bool(want_weights), bool(self.return_z),
                                torchops.EVENTS_HOOK(B, kc, kf) if torchops.EVENTS_HOOK else [],
-                               -1 if self.march_mode is None else int(self.march_mode))
+                               -1 if self.march_mode is None else int(self.march_mode), order)
         c_rgb, c_depth, c_w, f_rgb, f_depth, f_w, z_c, z_f = res
         outputs = DotMap(coarse=self._pack_out(c_w if want_weights else None, c_rgb, c_depth, sb, want_weights,
                                                z_c if self.return_z else None))
@@ -325,6 +380,19 @@ class NeRFRenderer(torch.nn.Module):
             outputs.fine = self._pack_out(f_w if want_weights else None, f_rgb, f_depth, sb, want_weights,
                                           z_f if self.return_z else None)
         return outputs
+
+    def _blocked_order(self, net):
+        if self.ray_order == "input":
+            return False
+        if self.ray_order == "blocked":
+            return True
+        if self.ray_order != "auto":
+            raise ValueError("ray_order must be 'auto', 'blocked' or 'input' (got %r)" % (self.ray_order,))
+        lat = getattr(net.encoder, "latent_cl", None)
+        if lat is None or lat.dim() != 4:
+            return False
+        stages = min(net.mlp_coarse.combine_layer, net.mlp_coarse.n_blocks) if hasattr(net.mlp_coarse, "n_blocks") else 1
+        return lat.shape[0] * lat.shape[1] * lat.shape[2] * 512 * 4 * max(stages, 1) > ORDER_AUTO_BYTES
 
     def _forward_callback(self, model, rays, sb, want_weights):
         """nerf.py:251-303 through the plug point ``model(points, coarse, viewdirs)``; sampling

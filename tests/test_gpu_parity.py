@@ -1154,6 +1154,65 @@ def test_fused_march_matches_unfused(precision, kc, kf, kfd, white, lindisp, n_v
                 assert torch.equal(o[p][k], b[p][k]), ("return_z=False", mode, p, k)
 
 
+@pytest.mark.parametrize("n_views,kc,kf,kfd,streams", [(3, 64, 64, 0, False), (1, 64, 64, 0, True),
+                                                       (1, 64, 32, 16, False), (3, 128, 64, 0, False)])
+def test_ray_order_is_bit_identical(n_views, kc, kf, kfd, streams):
+    """pnr_render_cfg.ray_order (ABI 8, NeRFRenderer.ray_order): the fused march taking the rays in
+    16 x 16 pixel blocks gives bit-identical outputs to the input order in march modes 1, 2 and 3,
+    with counter-mode draws (keyed by the ray's own index) and injected streams; the raw-output
+    path (mlp_fine None: the coarse march writes raw for the fine pass's reuse) too; an order with
+    out-of-range entries marches those units' own rays instead of faulting."""
+    import ctypes
+
+    from pnr import _lib, torchops, util
+    from pnr.renderer import ray_block_order
+
+    W, H = 64, 48
+    lat = synth.latent(10, n_views, 512, 30, 40)
+    poses = synth.srn_poses([30.0 * i for i in range(n_views)], radius=1.4).reshape(1, n_views, 4, 4)
+    focal = torch.tensor(60.0)
+    rays = util.gen_rays(synth.srn_poses([15.0], radius=1.4), W, H, focal, 0.4, 2.4).reshape(1, -1, 8).to(DEV)
+    order = ray_block_order(rays[0])
+    assert order is not None and not torch.equal(order.cpu(), torch.arange(W * H, dtype=torch.int32))
+    for fine_none in (False, True):
+        net = PixelNeRFNet(model_conf())
+        net.load_state_dict(synth.pixelnerf_state(1), strict=False)
+        if fine_none:
+            net.mlp_fine = None   # as eval_approx.py:62-63 does
+        net = net.to(DEV).eval()
+        net.encode_latent(lat.to(DEV), poses.to(DEV), focal.to(DEV), (W, H), num_objs=1)
+        r = NeRFRenderer(n_coarse=kc, n_fine=kf, n_fine_depth=kfd, depth_std=0.01, white_bkgd=True)
+        r.return_z = True
+        for mode in ((2,) if fine_none else (1, 2, 3)):
+            r.march_mode = mode
+            outs = []
+            for ro in ("input", "blocked"):
+                r.ray_order = ro
+                if streams:
+                    r.streams = synth.rng_streams(7, W * H, kc, kf, kfd)
+                with torch.no_grad():
+                    torch.manual_seed(3)
+                    outs.append(r(net, rays, want_weights=True))
+            torch.cuda.synchronize()
+            for p in ("coarse", "fine"):
+                for k in ("rgb", "depth", "weights", "z"):
+                    x, y = outs[0][p][k], outs[1][p][k]
+                    assert torch.equal(x, y), (mode, fine_none, p, k, float((x - y).abs().max()))
+    # out-of-range entries: those units march their own index (no fault, same result)
+    bad = order.clone()
+    bad[:5] = torch.tensor([-1, W * H, 2 ** 30, -7, W * H + 3], dtype=torch.int32, device=DEV)
+    bad[5:] = torch.arange(5, W * H, dtype=torch.int32, device=DEV)
+    ops_ = torchops.load()
+    desc, pc = net.hip_mlp(True)
+    res = []
+    for ro in (None, bad):
+        res.append(ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, pc, net.hip_proj(True),
+                                    None, rays[0].contiguous(), W * H, 64, 0, 0, 0.01, True, False, None, None, None,
+                                    None, 5, 0, True, False, [], 2, ro))
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(res[0], res[1]))
+
+
 def test_march_modes_in_two_host_threads():
     """calls are re-entrant with no mutable globals -- two host threads on one
     device (the DataParallel replicas of nerf.py:370 call from one thread each) render the

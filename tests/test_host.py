@@ -35,7 +35,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_error_channel():
     lib = _lib.load()
-    assert lib.pnr_abi_version() == 7
+    assert lib.pnr_abi_version() == 8
     assert lib.pnr_fold_batchnorm(None, 3, 10, None) == -1 and b"NULL" in lib.pnr_last_error()
     assert lib.pnr_latent_channels_last_backward(None, None, None, None, None, 1, 1, 4, 4, None) == -1
     assert b"NULL" in lib.pnr_last_error()
@@ -243,7 +243,7 @@ def test_render_cfg_march_mode_is_per_call():
     -1..3 is refused before any device work (host-side validation only: the pointers below
     are never dereferenced), and the refusal does not touch the process default."""
     lib = _lib.load()
-    assert ctypes.sizeof(_lib.RenderCfg) == 28
+    assert ctypes.sizeof(_lib.RenderCfg) == 40   # ABI 8: + ray_order (8-B aligned at 32)
     buf = ctypes.create_string_buffer(4096 + 16)
     p = ctypes.c_void_p((ctypes.addressof(buf) + 15) & ~15)   # 16-B aligned, never read
     sc = _lib.Scene(p, p, 1, 1, 4, 4, 512, 64.0, 64.0)
@@ -420,6 +420,52 @@ def test_built_device_code_passes_isa_lint():
     spec.loader.exec_module(lint)
     for f in files:
         assert lint.lint_file(f) == [], f
+
+
+def test_ray_block_order_groups_neighbouring_pixels():
+    """pnr.renderer.ray_block_order (the ray_order heuristic, ABI 8): on a pinhole camera's
+    row-major frame (util.gen_rays) it is a permutation whose every run of 256 consecutive rays
+    covers a compact pixel block (a row-major run spans 256 pixels of one or two rows); it keeps
+    the input order for rays without a common centre of projection; "auto" blocks only scenes
+    whose projected-latent rows exceed ORDER_AUTO_BYTES."""
+    from pnr import renderer as rmod
+    from pnr import util
+
+    W, H = 400, 300
+    rays = util.gen_rays(synth.srn_poses([10.0], phi=-12.0, radius=2.0), W, H, torch.tensor(300.0), 0.1, 5.0)
+    rays = rays.reshape(-1, 8)
+    order = rmod.ray_block_order(rays)
+    assert order.dtype == torch.int32 and torch.equal(torch.sort(order.long())[0], torch.arange(W * H))
+    ys, xs = order.long() // W, order.long() % W
+    spans = []
+    for i in range(0, W * H - 255, 256):
+        y, x = ys[i:i + 256], xs[i:i + 256]
+        spans.append(max(int(y.max() - y.min()), int(x.max() - x.min())))
+    spans.sort()
+    assert spans[len(spans) // 2] <= 40, spans[len(spans) // 2]   # ~16-32 px blocks, not 256-px rows
+    rnd = rays.clone()
+    rnd[:, :3] += torch.randn(W * H, 3)
+    assert rmod.ray_block_order(rnd) is None
+    assert rmod.ray_block_order(rays[:100]) is None
+
+    class Enc:
+        latent_cl = torch.empty(3, 150, 200, 512)
+
+    class Mlp:
+        combine_layer, n_blocks = 3, 5
+
+    class Net:
+        encoder, mlp_coarse = Enc(), Mlp()
+
+    r = rmod.NeRFRenderer()
+    assert r.ray_order == "auto" and r._blocked_order(Net())   # cfg4: 553 MB of projected rows
+    Net.encoder.latent_cl = torch.empty(1, 32, 32, 512)
+    assert not r._blocked_order(Net())                           # cfg3: 6 MB
+    r.ray_order = "blocked"
+    assert r._blocked_order(Net())
+    r.ray_order = "sideways"
+    with pytest.raises(ValueError):
+        r._blocked_order(Net())
 
 
 def _torchvision_resnet34_keys():

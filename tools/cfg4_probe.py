@@ -28,12 +28,14 @@ net.encode_latent(synth.latent(8, 3, 512, 150, 200).to(dev), sc["poses"][None].t
 rays = util.gen_rays(synth.srn_poses([10.0], phi=-12.0, radius=2.0).to(dev), 400, 300, sc["focal"], 0.1, 5.0,
                      c=sc["c"]).reshape(-1, 8)
 # ORDER: the frame's ray order -- "row" (gen_rays' row-major, gen_video's), "block:N" (N x N pixel
-# blocks, row-major inside and across blocks), "morton" (Z-order of the pixel coordinates)
+# blocks, row-major inside and across blocks), "morton" (Z-order of the pixel coordinates), "random"
 order = os.environ.get("ORDER", "row")
 if order != "row":
     yy, xx = torch.meshgrid(torch.arange(300), torch.arange(400), indexing="ij")
     yy, xx = yy.reshape(-1), xx.reshape(-1)
-    if order.startswith("block:"):
+    if order == "random":
+        key = torch.randperm(300 * 400, generator=torch.Generator().manual_seed(0))
+    elif order.startswith("block:"):
         nb = int(order.split(":")[1])
         key = ((yy // nb) * ((400 + nb - 1) // nb) + xx // nb) * nb * nb + (yy % nb) * nb + xx % nb
     else:
@@ -41,7 +43,8 @@ if order != "row":
         for bit in range(9):
             key |= ((xx >> bit) & 1) << (2 * bit) | ((yy >> bit) & 1) << (2 * bit + 1)
     rays = rays[torch.argsort(key).to(dev)].contiguous()
-r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=False, eval_batch_size=bench.RAY_BATCH).to(dev)
+r = NeRFRenderer(n_coarse=64, n_fine=64, white_bkgd=False,
+                 eval_batch_size=int(os.environ.get("EBS", bench.RAY_BATCH))).to(dev)
 r.ray_order = os.environ.get("RAY_ORDER", "auto")   # the renderer's processing order (ABI 8)
 dbg = getattr(_lib.load(), "pnr_debug_phase", None)
 ph = (ctypes.c_ulonglong * 32)()
@@ -55,7 +58,7 @@ with torch.no_grad():
         r(net, rays[None])
     torch.cuda.synchronize()
 print("cfg4 frame_ms %.2f" % ((time.perf_counter() - t0) / n * 1e3), os.environ.get("PNR_LIB_PATH", "default"), order,
-      "ray_order=" + r.ray_order, flush=True)
+      "ray_order=" + r.ray_order, "ebs=%d" % r.eval_batch_size, flush=True)
 if dbg is not None:
     dbg(ph, 0)
     v = list(ph)
