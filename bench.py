@@ -597,7 +597,7 @@ def composite_roofline(dev, ev, pmc_path=None, same_lease=False):
         for _ in range(2):
             ops.composite(z, raw, rays, True, want_weights=want_w)
         times = []
-        for _ in range(5):
+        for _ in range(11):   # the median of 11 launches (one launch varies by a few % on a box)
             ev.hip.hipEventRecord(evs[0], st)
             _lib.check(lib.pnr_composite(_lib.ptr(z), _lib.ptr(raw), _lib.ptr(rays), B, K, 1,
                                          _lib.ptr(w) if want_w else None, _lib.ptr(rgb),
