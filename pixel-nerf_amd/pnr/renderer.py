@@ -76,40 +76,38 @@ def ray_block_order(rays, block=16):
     view, so the scheduling units running at once on an XCD share its L2 (cfg4).
     The target camera is not known here: the image plane is the plane perpendicular to the mean
     direction, at unit distance, and the pixel rows' direction and pitch the median step between
-    consecutive rays (one pixel along a row for row-major input, gen_video's / eval's frames).  Returns an int32 (B,) permutation, or None when the rays
-    do not look like one pinhole camera's (then the input order is kept)."""
+    consecutive rays (one pixel along a row for row-major input, gen_video's / eval's frames).
+    Computed on the rays' device without a host synchronisation: an int32 (B,) permutation, the
+    input order itself when the rays do not look like one pinhole camera's; None below 4 blocks."""
     B = rays.shape[0]
     if B < 4 * block * block:
         return None
     o, d = rays[:, :3], rays[:, 3:6]
-    if float((o - o[:1]).abs().max()) > 1e-4 * (1.0 + float(o[0].abs().max())):
-        return None   # not one centre of projection
     axis = d.mean(0)
     axis = axis / axis.norm()
     cz = d @ axis
-    if float(cz.min()) <= 1e-3:
-        return None
     up = torch.zeros(3, device=d.device, dtype=d.dtype)
-    up[int(torch.argmin(axis.abs()))] = 1.0
+    up.scatter_(0, torch.argmin(axis.abs()).reshape(1), 1.0)
     e1 = torch.linalg.cross(axis, up)
     e1 = e1 / e1.norm()
     e2 = torch.linalg.cross(axis, e1)
-    t = d / cz[:, None]
+    t = d / cz.clamp_min(1e-3)[:, None]
     u, v = t @ e1, t @ e2
     # the pixel rows' direction and pitch: the median step between consecutive rays (one pixel
     # along a row for row-major input; the row wraps are outliers), so the blocks align with
     # the image's rows and columns
-    du, dv = float(torch.diff(u).median()), float(torch.diff(v).median())
-    pitch = (du * du + dv * dv) ** 0.5
-    if not pitch > 0.0:
-        return None
-    r1 = (e1 * du + e2 * dv) / pitch
+    du, dv = torch.diff(u).median(), torch.diff(v).median()
+    pitch = torch.sqrt(du * du + dv * dv)
+    r1 = (e1 * du + e2 * dv) / pitch.clamp_min(1e-30)
     r2 = torch.linalg.cross(axis, r1)
     u, v = t @ r1, t @ r2
-    cu = torch.floor((u - u.min()) / (block * pitch)).long()
-    cv = torch.floor((v - v.min()) / (block * pitch)).long()
-    key = cv * (int(cu.max()) + 1) + cu
-    return torch.argsort(key, stable=True).to(torch.int32)
+    cell = block * pitch.clamp_min(1e-30)
+    cu = torch.floor((u - u.min()) / cell).clamp(0, (1 << 20) - 1).long()
+    cv = torch.floor((v - v.min()) / cell).clamp(0, (1 << 20) - 1).long()
+    perm = torch.argsort((cv << 20) + cu, stable=True).to(torch.int32)
+    ok = ((o - o[:1]).abs().amax() <= 1e-4 * (1.0 + o[0].abs().amax())) & (cz.amin() > 1e-3) & (pitch > 0) & \
+        torch.isfinite(pitch)
+    return torch.where(ok, perm, torch.arange(B, device=rays.device, dtype=torch.int32))
 
 
 class NeRFRenderer(torch.nn.Module):
@@ -335,25 +333,31 @@ class NeRFRenderer(torch.nn.Module):
         # max_rays_per_call.  Several objects: one call, the scene record covers them all
         # (chunking inside each object would move the rays' counter-mode draw indices).
         step = max(1, min(int(self.max_rays_per_call), int(self.eval_batch_size))) if sb == 1 else max(B, 1)
+        starts = list(range(0, max(B, 1), step))
+        # every chunk's processing order before the first render is queued: the order's host
+        # decisions (ray_block_order) then never wait for a chunk in flight
+        orders = ([ray_block_order(rays[r0:min(B, r0 + step)]) for r0 in starts]
+                  if sb == 1 and self._blocked_order(net) else [None] * len(starts))
         parts = []
-        for r0 in range(0, max(B, 1), step):
+        for r0, order in zip(starts, orders):
             r1 = min(B, r0 + step)
             st = None if streams is None else tuple(t[r0:r1] for t in streams)
             if self.using_fine and kf == 0:
-                out = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, 0, 0, True, want_weights)
-                fine = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, 0, 0, False, want_weights)
+                out = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, 0, 0, True, want_weights, order)
+                fine = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, 0, 0, False, want_weights, order)
                 out.fine = fine.coarse
             else:
-                out = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, kf, kfd, True, want_weights)
+                out = self._fused_call(net, rays[r0:r1], sb, st, seed, r0, kc, kf, kfd, True, want_weights, order)
             parts.append(out)
         if len(parts) == 1:
             return parts[0]
         return DotMap({p: DotMap({k: torch.cat([o[p][k] for o in parts], 1) for k in parts[0][p]})
                        for p in parts[0]})
 
-    def _fused_call(self, net, rays, sb, streams, seed, offset, kc, kf, kfd, coarse, want_weights):
+    def _fused_call(self, net, rays, sb, streams, seed, offset, kc, kf, kfd, coarse, want_weights, order=None):
         """One torch.ops.pnr.render_rays call (pnr_render_forward_proj).  coarse=False: the
-        fine MLP in the coarse slot (a coarse-only march with the fine model)."""
+        fine MLP in the coarse slot (a coarse-only march with the fine model).  ``order``: the
+        processing order (pnr_render_cfg.ray_order) or None."""
         from . import torchops
 
         ops_ = torchops.load()
@@ -366,7 +370,6 @@ class NeRFRenderer(torch.nn.Module):
             u_c = u_f = u_j = n_d = None
         else:
             u_c, u_f, u_j, n_d = [t.contiguous() for t in streams]
-        order = ray_block_order(rays) if sb == 1 and self._blocked_order(net) else None
         res = ops_.render_rays(*torchops.scene_args(net), torchops.desc_list(desc), pc, pf, zc, zf, rays,
                                B // sb, kc, kf, kfd, float(self.depth_std), bool(self.white_bkgd),
                                bool(self.lindisp), u_c, u_f, u_j, n_d, int(seed or 0), int(offset),

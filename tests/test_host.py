@@ -425,8 +425,9 @@ def test_built_device_code_passes_isa_lint():
 def test_ray_block_order_groups_neighbouring_pixels():
     """pnr.renderer.ray_block_order (the ray_order heuristic, ABI 8): on a pinhole camera's
     row-major frame (util.gen_rays) it is a permutation whose every run of 256 consecutive rays
-    covers a compact pixel block (a row-major run spans 256 pixels of one or two rows); it keeps
-    the input order for rays without a common centre of projection; "auto" blocks only scenes
+    covers a compact pixel block (a row-major run spans 256 pixels of one or two rows), for the
+    frame and for gen_video's 50,000-ray chunks of it; it keeps the input order for rays without
+    a common centre of projection; "auto" blocks only scenes
     whose projected-latent rows exceed ORDER_AUTO_BYTES."""
     from pnr import renderer as rmod
     from pnr import util
@@ -443,9 +444,15 @@ def test_ray_block_order_groups_neighbouring_pixels():
         spans.append(max(int(y.max() - y.min()), int(x.max() - x.min())))
     spans.sort()
     assert spans[len(spans) // 2] <= 40, spans[len(spans) // 2]   # ~16-32 px blocks, not 256-px rows
+    for r0 in (0, 50000, 100000):   # gen_video's chunks (each a row-major band of the frame)
+        o = rmod.ray_block_order(rays[r0:r0 + 50000]).long() + r0
+        y, x = o // W, o % W
+        med = sorted(max(int(y[i:i + 256].max() - y[i:i + 256].min()), int(x[i:i + 256].max() - x[i:i + 256].min()))
+                     for i in range(0, len(o) - 255, 256))[len(o) // 512]
+        assert med <= 40, (r0, med)
     rnd = rays.clone()
-    rnd[:, :3] += torch.randn(W * H, 3)
-    assert rmod.ray_block_order(rnd) is None
+    rnd[:, :3] += torch.randn(W * H, 3)   # no common centre of projection: the input order
+    assert torch.equal(rmod.ray_block_order(rnd), torch.arange(W * H, dtype=torch.int32))
     assert rmod.ray_block_order(rays[:100]) is None
 
     class Enc:
