@@ -26,6 +26,8 @@ _BLOCK = re.compile(r"^(\.LBB\w+:|\s*; %bb\.\d+:)")
 _RESTORE = re.compile(r"^s_or_b64\s+exec,\s*exec,")
 _EXEC_WRITE = re.compile(r"^s_\w+\s+exec\b|^s_\w*saveexec\w*\s")
 _SPILL = re.compile(r"^(scratch_|v_accvgpr_(read|write)|buffer_(load|store)_\w+.*\boffen\b)")
+# a whole-wave section (SGPR spills to VGPR lanes): s_or_saveexec_b64 s[..], -1 ... s_mov_b64 exec, s[..]
+_WWM_ON = re.compile(r"^s_or_saveexec_b64\s+(s\[\d+:\d+\]),\s*-1\b")
 
 
 def lint_file(path):
@@ -34,19 +36,28 @@ def lint_file(path):
     fn = None
     pending = []      # spill / reload lines of the current block, before any EXEC write
     scanning = True   # no EXEC write seen yet in this block
+    wwm = None        # inside a whole-wave section: the SGPR pair that restores EXEC
     with open(path) as f:
         for n, raw in enumerate(f, 1):
             m = _FUNC.match(raw)
             if m and not raw.startswith(".L"):
-                fn, pending, scanning = m.group(1), [], True
+                fn, pending, scanning, wwm = m.group(1), [], True, None
                 continue
             if _BLOCK.match(raw):
-                pending, scanning = [], True
+                pending, scanning, wwm = [], True, None
                 continue
             ins = raw.split(";")[0].strip()
             if not ins or ins.startswith("."):
                 continue
             if not scanning:
+                continue
+            if wwm is not None:   # whole-wave spills are correct under any mask: skip the section
+                if re.match(r"^s_mov_b64\s+exec,\s*" + re.escape(wwm) + r"$", ins):
+                    wwm = None
+                continue
+            w = _WWM_ON.match(ins)
+            if w:
+                wwm = w.group(1)
                 continue
             if _RESTORE.match(ins):
                 hits += [(fn, ln, s, ins) for ln, s in pending]

@@ -402,6 +402,12 @@ def test_isa_lint_flags_a_spill_under_a_branch_mask(tmp_path):
     inside = tmp_path / "inside.s"   # a reload inside the region: its own mask write comes first
     inside.write_text(_LINT_BAD.replace("\ts_mov_b32 s20, s34\n", "\ts_and_saveexec_b64 s[8:9], vcc\n"))
     assert lint.lint_file(str(inside)) == []
+    wwm = tmp_path / "wwm.s"   # a whole-wave SGPR-spill section between the spill and the restore
+    wwm.write_text(_LINT_BAD.replace("\ts_or_b64 exec, exec, s[6:7]\n",
+                                     "\ts_or_saveexec_b64 s[10:11], -1\n\tscratch_store_dword off, v255, off\n"
+                                     "\ts_mov_b64 exec, s[10:11]\n\ts_or_b64 exec, exec, s[6:7]\n"))
+    hits = lint.lint_file(str(wwm))
+    assert len(hits) == 1 and "v5" in hits[0][2]
 
 
 def test_built_device_code_passes_isa_lint():
