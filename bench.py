@@ -733,7 +733,9 @@ def extra_configs(dev, precision, latent_proj=True, probe=None, oracle_rays=64):
     cfg4 = dict(rays_per_s=round(rays.shape[0] / s, 1), ms_per_frame=round(s * 1e3, 3),
                 gflop_per_ray=round(192 * flop_per_point(3, False) / 1e9, 4),
                 workload="cfg4: DTU 400x300 frame, 3 source views (150x200 latent each), 64 + 64, "
-                         "gen_video's %d-ray chunks" % RAY_BATCH)
+                         "gen_video's %d-ray chunks" % RAY_BATCH,
+                ray_order="%s (%s)" % (r.ray_order, "16 x 16 pixel blocks: the projected rows exceed the caches"
+                                       if r._blocked_order(net) else "input order"))
     if probe is not None:
         probe.on = False
         avg, roof = probe.summary(precision, latent_proj, ns=3)
